@@ -1,0 +1,213 @@
+"""Discrete-KG throughput on MI355X (BASELINE.json headline metric).
+
+One step = one DiscreteKnowledgeGradient forward over a batch of B candidates
+per GPU (the reference's ``forward(X[B,1,d])``, discretekg.py:131-159) at the
+headline workload: m=2 outputs, n_train=256, n_disc=1024 (32x32 std grid),
+S=16 scalarisations, B=128 candidates per GPU, d=2, fp64.  Inputs and GP state
+are resident in HBM before timing.  For N>1 (torchrun, one rank per GPU,
+RCCL) each rank evaluates its own 128 candidates (weak scaling) and the
+per-candidate KG values are all-gathered every step (async, double
+buffered), so every rank ends with the whole batch.
+
+Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus the
+roofline of the dominant kernel (HIP-event timed, same stream) and a bounded
+CPU baseline of the oracle restatement on the host cores.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "decoupled-kg_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="headline")
+    ap.add_argument("--target", type=int, default=None, help="target_output_ix (decoupled path); default full")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--profile-reps", type=int, default=50)
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_headline.json"),
+                    help="per-kernel HBM traffic from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
+    return ap.parse_args()
+
+
+def stage_model(w, m, n, N, B, S, d):
+    """Algorithmic flops / HBM bytes per launch of each kernel (DESIGN.md 'Roofline')."""
+    kev = 3 * d + 8  # flops per kernel evaluation (distance + Matern profile)
+    fl_cross = sum(B * nn * (nn + 1) + 2 * B * nn + B * nn * kev for nn in n)
+    fl_cov = sum(2 * B * N * nn + B * N * kev for nn in n)
+    fl_env = B * S * (N + 1) * (4 * m + 2)
+    by_cross = sum(8 * (nn * nn + nn * d + B * nn + B) for nn in n) + 8 * B * d
+    by_cov = sum(8 * (B * nn + N * nn + B * N) for nn in n) + 8 * (B + N) * d
+    by_env = 8 * (m * (N + B * N + B) + S * m + B)
+    return {"cross_root_kernel": (fl_cross, by_cross), "posterior_cov_kernel": (fl_cov, by_cov),
+            "envelope_kernel": (fl_env, by_env)}
+
+
+def cpu_baseline(model, D, W, X, target, seconds, threads):
+    """The oracle's structure-faithful restatement of the reference path on host cores."""
+    from oracle.discretekg import calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output
+    from oracle.gp import ModelList, OutputGP
+
+    torch.set_num_threads(threads)
+    om = ModelList([OutputGP(m.train_x, m.train_y, m.lengthscale, m.outputscale, m.noise, m.mean_constant,
+                             m.kernel, m.nu, m.y_mean, m.y_std) for m in model.models])
+    Xc = X.cpu()
+
+    def one(x):
+        if target is None:
+            return calculate_discrete_kg(om, x, D, W)
+        return calculate_discrete_kg_conditioning_on_single_output(om, x, target, D, W)
+
+    one(Xc[0])  # warm-up (builds the per-model caches, as GPyTorch does on first call)
+    t0 = time.perf_counter()
+    cnt = 0
+    while cnt < Xc.shape[0] and (time.perf_counter() - t0 < seconds or cnt < 4):
+        one(Xc[cnt])
+        cnt += 1
+    dt = time.perf_counter() - t0
+    return {"value": cnt / dt, "unit": "KG-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{cnt} of the {Xc.shape[0]} headline candidates, one forward each (per-candidate loop, "
+                      f"dense (N+1)^2 posterior covariance, reference epigraph walk; torch fp64 CPU), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    w = WORKLOADS[args.workload]
+    model, D, X0, W = make_problem(w)
+    # weak scaling: every rank evaluates its own B candidates (Sobol stream per rank)
+    X = torch.quasirandom.SobolEngine(w.d, scramble=True, seed=4 + 1000 * rank).draw(w.B, dtype=torch.double)
+    if rank == 0:
+        X = X0
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=args.target, device=dev)
+    state = acq._state
+    Xd = X.to(dev).contiguous()
+    Wd = W.to(dev)
+    gathered = [torch.empty(world * w.B, dtype=torch.double, device=dev) for _ in range(2)]
+    works = [None, None]
+
+    def step(k):
+        kg = state.forward(Xd, Wd, args.target)
+        if world > 1:
+            slot = k % 2
+            if works[slot] is not None:
+                works[slot].wait()
+            works[slot] = dist.all_gather_into_tensor(gathered[slot], kg, async_op=True)
+        return kg
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for k in range(args.steps):
+        step(k)
+    for wk in works:
+        if wk is not None:
+            wk.wait()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    t = torch.tensor([max(wall, gpu_s)], dtype=torch.double, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t)
+    value = world * w.B * args.steps / elapsed
+
+    # ---- per-kernel durations (HIP events on the launch stream), roofline of the dominant kernel
+    names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
+    acc = [0.0, 0.0, 0.0]
+    for _ in range(args.profile_reps):
+        _, ms = state.forward(Xd, Wd, args.target, timed=True)
+        acc = [a + b for a, b in zip(acc, ms)]
+    avg_ms = [a / args.profile_reps for a in acc]
+    model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)
+    dom = max(range(3), key=lambda i: avg_ms[i])
+    fl, by = model_fb[names[dom]]
+    if names[dom] == "posterior_cov_kernel":
+        bound, ach, peak, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        bound, ach, peak, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            traffic = json.load(open(args.pmc)).get(names[dom], {}).get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+    roof = {"kernel": names[dom], "bound": bound, "achieved": ach, "peak": peak, "unit": unit,
+            "frac": ach / peak, "traffic": traffic, "algorithmic_flops": fl, "algorithmic_bytes": by,
+            "avg_launch_us": avg_ms[dom] * 1e3,
+            "stages_us": {n: a * 1e3 for n, a in zip(names, avg_ms)}}
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if args.cpu_seconds > 0 and world == 1:
+            cpu = cpu_baseline(model, D, W, X0, args.target, args.cpu_seconds, args.cpu_threads)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "KG-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: seeded GP-prior draw, lengthscales family (l=0.2/1.8, s=1/50, noise 1e-4)",
+            "config": {"workload": args.workload, "m": w.m, "n_train": w.n_train, "n_disc": D.shape[0],
+                       "S": w.S, "B_per_gpu": w.B, "d": w.d,
+                       "path": "full" if args.target is None else f"target_output_ix={args.target}",
+                       "parallelism": f"candidates sharded over {world} GPU(s); per-step async all-gather"},
+            "forward_calls_per_s": world * args.steps / elapsed,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

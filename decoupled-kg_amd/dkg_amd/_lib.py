@@ -1,0 +1,102 @@
+"""ctypes binding of ``libdkg.so`` (C ABI in ``include/dkg.h``).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly
+when the shared object is missing, and every entry point raises on a non-zero
+status with the library's own message.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_size_t, c_void_p
+
+from .errors import BotorchTensorDimensionError, DkgNativeError, UnsupportedError
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdkg.so")
+
+ABI_VERSION = 1
+MAX_OUTPUTS = 8
+MAX_DIM = 16
+
+DKG_OK, DKG_ERR_ARG, DKG_ERR_UNSUPPORTED, DKG_ERR_WORKSPACE, DKG_ERR_HIP, DKG_ERR_NO_LINES = range(6)
+
+
+class DkgOutput(ctypes.Structure):
+    """``struct dkg_output`` (include/dkg.h)."""
+
+    _fields_ = [
+        ("n", c_int32),
+        ("kernel", c_int32),
+        ("outputscale", c_double),
+        ("noise", c_double),
+        ("mean_constant", c_double),
+        ("y_mean", c_double),
+        ("y_std", c_double),
+        ("inv_lengthscale", c_void_p),
+        ("train_x", c_void_p),
+        ("alpha", c_void_p),
+        ("root_frag", c_void_p),
+        ("disc_frag", c_void_p),
+        ("disc_mean", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/dkg.h declares.
+SIGNATURES = {
+    "dkg_abi_version": (c_int, []),
+    "dkg_last_error": (c_char_p, []),
+    "dkg_frag_elems": (c_size_t, [c_int, c_int]),
+    "dkg_kernel_matrix": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_int, c_double,
+                                  c_void_p, c_void_p]),
+    "dkg_pack_root": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    "dkg_cross_root": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_forward_workspace": (c_size_t, [POINTER(DkgOutput), c_int, c_int, c_int, c_int]),
+    "dkg_forward": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
+                            c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dkg_forward_timed": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                  c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
+                                  POINTER(c_float)]),
+    "dkg_lines_kg": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_debug_mfma_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load and type the native library once (raises DkgNativeError if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DkgNativeError(
+            f"libdkg.so not found at {LIB_PATH}; build it with `make -C decoupled-kg_amd` "
+            f"(or __graft_entry__.build()).  There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.dkg_abi_version() != ABI_VERSION:
+        raise DkgNativeError(f"libdkg.so ABI {lib.dkg_abi_version()} != expected {ABI_VERSION}; rebuild it")
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status == DKG_OK:
+        return
+    msg = f"{what}: {load().dkg_last_error().decode(errors='replace')}"
+    if status == DKG_ERR_ARG:
+        raise BotorchTensorDimensionError(msg)
+    if status == DKG_ERR_UNSUPPORTED:
+        raise UnsupportedError(msg)
+    if status == DKG_ERR_NO_LINES:
+        raise ValueError(msg)
+    raise DkgNativeError(msg)
+
+
+def ptr(t) -> int:
+    """Device address of a tensor (0 for None)."""
+    return 0 if t is None else int(t.data_ptr())

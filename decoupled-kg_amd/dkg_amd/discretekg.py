@@ -1,0 +1,211 @@
+"""Discrete multi-objective knowledge gradient on MI355X — drop-in host mirror.
+
+Same surface as the reference's
+``decoupledbo.modules.acquisition.discretekg`` (``discretekg.py:25-338``):
+
+* ``DiscreteKnowledgeGradient(model, x_discretisation, scalarisation_weights=None,
+  target_output_ix=None)`` with ``create_with_sobol_sample``, ``set_X_pending``
+  and ``forward(X[*batch, 1, d]) -> [*batch]`` (``:33-159``);
+* ``calculate_discrete_kg`` (``:162-235``) and
+  ``calculate_discrete_kg_conditioning_on_single_output`` (``:238-338``);
+* ``kg_from_lines`` — the epigraph + expectation stage
+  (``calculate_epigraph_indices`` + ``calculate_expected_value_of_piecewise_linear_function``
+  + ``- max(intercepts)``, ``:225-233, 341-452``) batched on the device.
+
+The fitted GP state lives in HBM (``gp_state.DeviceGPState``); every forward
+is three HIP kernel launches through the C ABI (``include/dkg.h``).  There is
+no CPU fallback: without the HIP library or a ROCm device these raise.
+"""
+
+from __future__ import annotations
+
+from functools import wraps
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from .errors import BotorchTensorDimensionError, UnsupportedError
+from .gp_state import DeviceGPState, current_stream_ptr
+from .model import ModelListGPState, SingleTaskGPState, from_botorch
+
+try:  # pragma: no cover - BoTorch is not installed in this image
+    from botorch.acquisition import AcquisitionFunction as _Base  # type: ignore
+
+    _HAVE_BOTORCH = True
+except Exception:  # noqa: BLE001
+    _Base = torch.nn.Module
+    _HAVE_BOTORCH = False
+
+
+def t_batch_mode_transform(expected_q: Optional[int] = None):
+    """BoTorch ``t_batch_mode_transform`` (as used at ``discretekg.py:131``)."""
+
+    def decorator(method):
+        @wraps(method)
+        def decorated(acqf, X, *args, **kwargs):
+            if not isinstance(X, Tensor):
+                return method(acqf, X, *args, **kwargs)
+            if X.dim() < 2:
+                raise ValueError(
+                    f"{type(acqf).__name__} requires X to have at least 2 dimensions,"
+                    f" but received X with only {X.dim()} dimensions.")
+            if expected_q is not None and X.shape[-2] != expected_q:
+                raise AssertionError(
+                    f"Expected X to be `batch_shape x q={expected_q} x d`, but got X with shape {X.shape}.")
+            X = X if X.dim() > 2 else X.unsqueeze(0)
+            return method(acqf, X, *args, **kwargs)
+
+        return decorated
+
+    return decorator
+
+
+def _as_model_state(model) -> ModelListGPState:
+    if isinstance(model, ModelListGPState):
+        return model
+    if isinstance(model, SingleTaskGPState):
+        return ModelListGPState(model)
+    return from_botorch(model)
+
+
+class _ForwardFn(torch.autograd.Function):
+    """Device forward; the closed-form backward is not wired in yet."""
+
+    @staticmethod
+    def forward(ctx, X, state, W, target):
+        return state.forward(X, W, target)
+
+    @staticmethod
+    def backward(ctx, grad):  # pragma: no cover
+        raise NotImplementedError("DiscreteKnowledgeGradient backward (dKG/dX) is not implemented yet")
+
+
+class DiscreteKnowledgeGradient(_Base):
+    """Discrete knowledge gradient (C-MOKG), linear scalarisations only."""
+
+    @classmethod
+    def create_with_sobol_sample(cls, model, bounds: Tensor, num_discrete_points: int,
+                                 scalarisation_weights: Optional[Tensor] = None,
+                                 target_output_ix: Optional[int] = None):
+        """Sobol discretisation (``discretekg.py:33-60``, ``draw_sobol_samples(bounds, N, q=1)``)."""
+        d = bounds.shape[-1]
+        eng = torch.quasirandom.SobolEngine(d, scramble=True)
+        raw = eng.draw(num_discrete_points, dtype=bounds.dtype).to(bounds.device)
+        x_disc = bounds[0] + (bounds[1] - bounds[0]) * raw
+        return cls(model, x_disc, scalarisation_weights, target_output_ix)
+
+    def __init__(self, model, x_discretisation: Tensor, scalarisation_weights: Optional[Tensor] = None,
+                 target_output_ix: Optional[int] = None, device=None):
+        if _HAVE_BOTORCH:  # pragma: no cover
+            super().__init__(model=model)
+        else:
+            super().__init__()
+            self.model = model
+        state = _as_model_state(model)
+        if x_discretisation.dim() != 2:
+            raise BotorchTensorDimensionError(
+                f"Expected 'x_discretisation' to have two dimensions. "
+                f"Got {x_discretisation.dim()=}.")
+        if scalarisation_weights is None:
+            if state.num_outputs != 1:
+                raise UnsupportedError("Models with more than one output must specify 'scalarisation_weights'.")
+            scalarisation_weights = torch.tensor([[1.0]]).to(x_discretisation)
+        if scalarisation_weights.dim() != 2:
+            raise BotorchTensorDimensionError(
+                f"Expected 'scalarisation_weights' to have two dimensions: The first "
+                f"indexing different scalarisations to be averaged over and the second "
+                f"indexing coordinates of the objective space. "
+                f"Got {scalarisation_weights.dim()=}")
+        if scalarisation_weights.shape[-1] != state.num_outputs:
+            raise BotorchTensorDimensionError(
+                f"Expected the last dimension of 'scalarisation_weights' to have one "
+                f"element per objective. Got {scalarisation_weights.shape[-1]=} != "
+                f"{state.num_outputs}=model.num_outputs.")
+        if target_output_ix is not None and not (0 <= int(target_output_ix) < state.num_outputs):
+            raise BotorchTensorDimensionError(
+                f"target_output_ix={target_output_ix} out of range for {state.num_outputs} outputs")
+        self.x_discretisation = x_discretisation
+        self.scalarisation_weights = scalarisation_weights
+        self.target_output_ix = target_output_ix
+        self._state = DeviceGPState(state, x_discretisation, device)
+        self._W = scalarisation_weights.detach().to(self._state.device, torch.double).contiguous()
+
+    def set_X_pending(self, X_pending: Optional[Tensor] = None) -> None:
+        raise UnsupportedError(f"{type(self).__name__} does not account for X_pending yet.")
+
+    @t_batch_mode_transform(expected_q=1)
+    def forward(self, X: Tensor) -> Tensor:
+        batch_shape, d = X.shape[:-2], X.shape[-1]
+        if d != self.x_discretisation.shape[-1]:
+            raise RuntimeError(
+                f"Expected X to have last dimension matching 'self.x_discretisation'. "
+                f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
+        flat = X.reshape(-1, d)
+        kg = _ForwardFn.apply(flat, self._state, self._W, self.target_output_ix)
+        return kg.to(device=X.device, dtype=X.dtype).reshape(batch_shape)
+
+    def forward_pairs(self, X: Tensor) -> Tensor:
+        """KG per (candidate, scalarisation): [B, S] (the per-``j`` values of ``:200-233``)."""
+        flat = X.reshape(-1, X.shape[-1])
+        pairs = torch.empty(flat.shape[0], self._W.shape[0], dtype=torch.double, device=self._state.device)
+        self._state.forward(flat, self._W, self.target_output_ix, kg_pairs=pairs)
+        return pairs
+
+
+def _check_weights(w: Tensor) -> None:
+    if w.dim() != 2:
+        raise BotorchTensorDimensionError(
+            "Expected 'scalarisation_weights' to have two dimensions: The first "
+            "indexing different scalarisations to be averaged over and the second "
+            "indexing coordinates of the objective space.")
+
+
+def calculate_discrete_kg(model, xnew: Tensor, discretisation: Tensor, scalarisation_weights: Tensor) -> Tensor:
+    """KG at one candidate, all outputs observed (``discretekg.py:162-235``)."""
+    _check_weights(scalarisation_weights)
+    acq = DiscreteKnowledgeGradient(model, discretisation, scalarisation_weights)
+    return acq(xnew.reshape(1, 1, -1)).reshape(())
+
+
+def calculate_discrete_kg_conditioning_on_single_output(model, xnew: Tensor, obj_idx_new: int,
+                                                        discretisation: Tensor,
+                                                        scalarisation_weights: Tensor) -> Tensor:
+    """KG at one candidate observing output ``obj_idx_new`` only (``discretekg.py:238-338``)."""
+    _check_weights(scalarisation_weights)
+    state = _as_model_state(model)
+    if not isinstance(state, ModelListGPState):
+        raise UnsupportedError(f"Input 'model' must be a 'ModelListGP'. Got {type(model)=}.")
+    acq = DiscreteKnowledgeGradient(state, discretisation, scalarisation_weights, target_output_ix=obj_idx_new)
+    return acq(xnew.reshape(1, 1, -1)).reshape(())
+
+
+def kg_from_lines(intercepts: Tensor, slopes: Tensor, return_hull_size: bool = False):
+    """E[max_k (a_k + b_k Z)] - max_k a_k per set of lines, on the device.
+
+    ``intercepts``/``slopes``: [..., L] (same shape).  Batched form of the
+    reference's epigraph + expectation + baseline (``discretekg.py:225-233``).
+    """
+    if intercepts.shape != slopes.shape:
+        raise BotorchTensorDimensionError(
+            f"Expected 'intercepts' and 'slopes' to have the same shape. "
+            f"Got {intercepts.shape=} and {slopes.shape=}.")
+    if intercepts.dim() < 1:
+        raise BotorchTensorDimensionError("Expected 'intercepts' and 'slopes' to have at least one dimension.")
+    L = intercepts.shape[-1]
+    if L == 0:
+        raise ValueError(f"Expected inputs to specify at least one line. Got intercepts.shape[-1]={L}.")
+    lib = _lib.load()
+    dev = intercepts.device if intercepts.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    a = intercepts.detach().to(dev, torch.double).reshape(-1, L).contiguous()
+    b = slopes.detach().to(dev, torch.double).reshape(-1, L).contiguous()
+    P = a.shape[0]
+    kg = torch.empty(P, dtype=torch.double, device=dev)
+    hull = torch.empty(P, dtype=torch.int32, device=dev) if return_hull_size else None
+    _lib.check(lib.dkg_lines_kg(_lib.ptr(a), _lib.ptr(b), P, L, _lib.ptr(kg), _lib.ptr(hull),
+                                current_stream_ptr(dev)), "dkg_lines_kg")
+    out = kg.reshape(intercepts.shape[:-1]).to(intercepts.device)
+    if return_hull_size:
+        return out, hull.reshape(intercepts.shape[:-1]).to(intercepts.device)
+    return out

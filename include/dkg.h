@@ -1,0 +1,139 @@
+/*
+ * dkg.h — C ABI of the MI355X-native Discrete Knowledge Gradient hot path.
+ *
+ * The reference (quasirandom/decoupled-kg, pure Python) computes the discrete
+ * multi-objective KG in
+ *   src/decoupledbo/modules/acquisition/discretekg.py
+ *     DiscreteKnowledgeGradient.forward                       :131-159
+ *     calculate_discrete_kg                                    :162-235
+ *     calculate_discrete_kg_conditioning_on_single_output      :238-338
+ *     calculate_epigraph_indices                               :341-412
+ *     calculate_expected_value_of_piecewise_linear_function    :415-452
+ * on top of BoTorch/GPyTorch exact GP posteriors (model.posterior at
+ * :182-185 and :275-284; model family src/decoupledbo/modules/model/factory.py).
+ *
+ * This library replaces that arithmetic with hand-written HIP kernels for
+ * gfx950.  Plain pointers and sizes only; every pointer marked "device" is a
+ * device allocation owned by the caller; every entry point is stream ordered
+ * on `stream` (a hipStream_t, NULL = legacy default stream) and never
+ * synchronises unless its name says "timed".  Status codes instead of
+ * exceptions; dkg_last_error() returns a thread-local message.
+ *
+ * Data layout in HBM (see DESIGN.md "Data layout"):
+ *   n_pad(n) = n rounded up to a multiple of 16.
+ *   A "fragment-packed" matrix P (rows x n, rows padded to 16) is stored as
+ *   F[t][kb][l] = P[16 t + (l & 15)][4 kb + (l >> 4)],  t < rows_pad/16,
+ *   kb < n_pad/4, l < 64 — exactly the per-lane operand order of
+ *   v_mfma_f64_16x16x4_f64, so every MFMA operand load is one coalesced
+ *   512-byte read.  Padding entries are zero.
+ */
+#ifndef DKG_AMD_DKG_H
+#define DKG_AMD_DKG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DKG_ABI_VERSION 1
+#define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
+#define DKG_MAX_DIM 16      /* input dimension d */
+
+enum dkg_status {
+  DKG_OK = 0,
+  DKG_ERR_ARG = 1,          /* bad argument / shape (reference raises BotorchTensorDimensionError) */
+  DKG_ERR_UNSUPPORTED = 2,  /* outside supported sizes (reference: UnsupportedError) */
+  DKG_ERR_WORKSPACE = 3,    /* workspace too small */
+  DKG_ERR_HIP = 4,          /* HIP runtime error */
+  DKG_ERR_NO_LINES = 5      /* no lines (reference: ValueError, discretekg.py:466-470) */
+};
+
+/* Covariance families of model/factory.py:116 (ScaleKernel(base)). */
+enum dkg_kernel { DKG_MATERN12 = 0, DKG_MATERN32 = 1, DKG_MATERN52 = 2, DKG_RBF = 3 };
+
+/* Fitted state of one output GP (one SingleTaskGP of the ModelListGP,
+ * factory.py:63-88) plus its caches over the discretisation.  The caches are
+ * the quantities GPyTorch keeps for exact prediction with fast_pred_var:
+ * R = L^{-T} with L = chol(K_XX + noise I), alpha = (K_XX + noise I)^{-1}(y - c). */
+typedef struct dkg_output {
+  int32_t n;                 /* training points */
+  int32_t kernel;            /* enum dkg_kernel */
+  double outputscale;        /* ScaleKernel outputscale s */
+  double noise;              /* likelihood noise variance (model space) */
+  double mean_constant;      /* ConstantMean c */
+  double y_mean, y_std;      /* Standardize(m=1) untransform (0, 1 if absent) */
+  const double* inv_lengthscale; /* device [d]: 1 / ARD lengthscale */
+  const double* train_x;     /* device [n x d] row-major (normalised inputs) */
+  const double* alpha;       /* device [n_pad(n)], zero padded */
+  const double* root_frag;   /* device, fragment-packed R^T view: F[tj][kb][l] = R[4kb+(l>>4)][16tj+(l&15)], n_pad^2 */
+  const double* disc_frag;   /* device, fragment-packed Q_D = K(D,X) R: N_pad x n_pad (nullable for dkg_cross_root) */
+  const double* disc_mean;   /* device [N]: c + K(D,X) alpha, model space (nullable for dkg_cross_root) */
+} dkg_output;
+
+int dkg_abi_version(void);
+const char* dkg_last_error(void);
+
+/* Number of doubles of a fragment-packed (rows x n) matrix: n_pad(rows)*n_pad(n). */
+size_t dkg_frag_elems(int rows, int n);
+
+/* out[i*n2+j] = s*k(x1_i, x2_j) (+ diag_add on i==j when n1==n2).
+ * Replaces the covariance evaluation of ScaleKernel(Matern|RBF) (factory.py:110-135,
+ * GPyTorch Kernel.forward) used to build K_XX + noise I for the Cholesky. */
+int dkg_kernel_matrix(const dkg_output* o, int d, const double* x1, int n1, const double* x2, int n2,
+                      double diag_add, double* out, void* stream);
+
+/* Pack dense row-major R (n x n, device) into o->root_frag layout (device). */
+int dkg_pack_root(const double* r, int n, double* root_frag, void* stream);
+
+/* Q = K(x, X) R (fragment-packed, rows x n) and mean = c + K(x, X) alpha (model
+ * space, nullable).  This is the test-train half of GPyTorch's exact
+ * prediction (DefaultPredictionStrategy mean_cache / covar_cache products)
+ * behind model.posterior (discretekg.py:182-185, :275-284).  With x = the
+ * discretisation D it builds disc_frag / disc_mean. */
+int dkg_cross_root(const dkg_output* o, int d, const double* x, int rows, double* q_frag,
+                   double* mean, void* stream);
+
+/* Bytes of scratch dkg_forward needs for (m outputs, N points, B candidates, S weights). */
+size_t dkg_forward_workspace(const dkg_output* outs, int m, int N, int B, int S);
+
+/* Discrete KG for B candidates: kg[b] = mean_j KG(xnew_b, w_j).
+ * Replaces DiscreteKnowledgeGradient.forward (discretekg.py:131-159) with
+ * target = -1 -> calculate_discrete_kg (:162-235, coupled evaluation),
+ * target = t  -> calculate_discrete_kg_conditioning_on_single_output (:238-338).
+ *   outs    : m output states (host array of structs holding device pointers)
+ *   disc    : device [N x d] discretisation (x_discretisation)
+ *   xnew    : device [B x d] candidates
+ *   weights : device [S x m] linear scalarisation weights
+ *   kg      : device [B] output
+ *   kg_pairs: device [B x S] per-(candidate, scalarisation) KG, nullable
+ *   workspace: device scratch of dkg_forward_workspace() bytes */
+int dkg_forward(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew,
+                int B, const double* weights, int S, int target, double* kg, double* kg_pairs,
+                void* workspace, size_t workspace_bytes, void* stream);
+
+/* As dkg_forward, but records HIP events around each of the three kernels on
+ * `stream`, synchronises, and returns their durations in ms:
+ * stage_ms[0] = cross (K(x,X) R), [1] = posterior covariance GEMM, [2] = envelope + expectation. */
+int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew,
+                      int B, const double* weights, int S, int target, double* kg, double* kg_pairs,
+                      void* workspace, size_t workspace_bytes, void* stream, float* stage_ms);
+
+/* Envelope stage alone: for P independent sets of L lines a_k + b_k z
+ * (device, row-major [P][L]) kg[p] = E[max_k (a_k + b_k Z)] - max_k a_k, Z ~ N(0,1),
+ * and optionally the number of upper-envelope lines n_hull[p] (nullable).
+ * Replaces calculate_epigraph_indices + calculate_expected_value_of_piecewise_
+ * linear_function + the baseline subtraction (discretekg.py:225-233, 341-452);
+ * L = 0 -> DKG_ERR_NO_LINES (the reference's ValueError, :466-470). */
+int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,
+                 void* stream);
+
+/* Debug/self-test: C[16x16] = A[16x4] B[4x16] (row-major, device) with one
+ * v_mfma_f64_16x16x4_f64 using the operand/result lane maps the kernels assume. */
+int dkg_debug_mfma_f64(const double* a, const double* b, double* c, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DKG_AMD_DKG_H */

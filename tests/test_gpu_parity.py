@@ -1,0 +1,299 @@
+"""HIP path vs the CPU oracle on identical inputs (needs a real MI355X).
+
+Every check goes through the C ABI (``include/dkg.h``) via ``dkg_amd``.
+Tolerance: |KG_gpu - KG_oracle| <= 1e-6 |KG_oracle| + floor, the floor being
+the fp64 rounding bound of ``helpers.rounding_floor``.
+"""
+
+import math
+
+import pytest
+import torch
+
+from helpers import assert_kg_close, rounding_floor, to_oracle, to_state
+from oracle.discretekg import (
+    _kg_from_lines,
+    calculate_discrete_kg,
+    calculate_discrete_kg_conditioning_on_single_output,
+    discrete_kg_batched,
+    discrete_kg_forward,
+    lines_batched,
+)
+from oracle.fit import make_reference_test_model, reference_test_discretisation
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TRIO = [[0.7, 0.3], [0.6, 0.4], [0.5, 0.5]]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def test_mfma_f64_lane_maps():
+    from dkg_amd import _lib
+
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(0)
+    A = torch.randint(-8, 8, (16, 4), generator=g).double()
+    Bm = torch.randint(-8, 8, (4, 16), generator=g).double()
+    a, b = A.to(DEV), Bm.to(DEV)
+    c = torch.empty(16, 16, dtype=torch.double, device=DEV)
+    _lib.check(lib.dkg_debug_mfma_f64(_lib.ptr(a), _lib.ptr(b), _lib.ptr(c), 0), "debug")
+    torch.cuda.synchronize()
+    assert torch.equal(c.cpu(), A @ Bm)
+
+
+# ---------------------------------------------------------------- envelope stage
+def _oracle_lines_kg(a, b):
+    return torch.stack([_kg_from_lines(a[p], b[p]) for p in range(a.shape[0])])
+
+
+# reference epigraph / expectation KAT line sets (test_discretekg.py:150-327)
+KAT_SETS = [
+    ([1.0, 1.5], [0.0, 0.0]),
+    ([1.5], [-1.9]),
+    ([1.5, 0.0], [-0.5, 0.0]),
+    ([0.0, 1.5], [0.0, -0.5]),
+    ([0.0, 0.0, -0.5, 0.0], [-1.0, -1.0, 0.0, 1.5]),
+    ([0.0, -1.0, 0.0], [-2.0, -1.0, 0.0]),
+    ([-1.0, 0.0, 0.0], [-1.0, 0.0, -2.0]),
+    ([1.5, 0.0], [0.0, 1e-12]),
+    ([1.5, 0.0], [-0.5, -0.5]),
+    ([0.0, 0.0], [0.0, 1.0]),
+]
+
+
+@pytest.mark.parametrize("idx", range(len(KAT_SETS)))
+def test_lines_kg_reference_kats(idx):
+    from dkg_amd import kg_from_lines
+
+    a, b = (torch.tensor(v, dtype=torch.double) for v in KAT_SETS[idx])
+    got = kg_from_lines(a.to(DEV), b.to(DEV)).cpu()
+    ref = _kg_from_lines(a, b)
+    assert abs(float(got) - float(ref)) <= 1e-12 + 1e-9 * abs(float(ref))
+
+
+def test_lines_kg_relu_exact():
+    from dkg_amd import kg_from_lines
+
+    got = kg_from_lines(torch.tensor([0.0, 0.0], device=DEV), torch.tensor([0.0, 1.0], device=DEV))
+    assert abs(float(got) - 1 / math.sqrt(2 * math.pi)) < 1e-15
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 17, 64, 65, 200, 1025, 2112])
+def test_lines_kg_random_sets(L):
+    from dkg_amd import kg_from_lines
+
+    g = torch.Generator().manual_seed(L)
+    P = 64
+    a = torch.randn(P, L, generator=g, dtype=torch.double)
+    b = torch.randn(P, L, generator=g, dtype=torch.double)
+    b[:4] = 0.0                       # short-circuit sets
+    b[4:8] = b[4:8].round()           # many equal slopes
+    a[8:12] = a[8:12].round()         # many equal intercepts
+    b[12:14] = 1e-10 * b[12:14]       # |b| < 1e-9 everywhere
+    got = kg_from_lines(a.to(DEV), b.to(DEV)).cpu()
+    ref = _oracle_lines_kg(a, b)
+    floor = 64 * torch.finfo(torch.double).eps * a.abs().amax(-1)
+    assert_kg_close(got, ref, floor)
+    assert bool((got >= 0).all())
+
+
+def test_lines_kg_parabola_many_hull_lines():
+    """Every line on the envelope (tangents of a parabola): survivor overflow path."""
+    from dkg_amd import kg_from_lines
+
+    L = 1025
+    s = torch.linspace(-3, 3, L, dtype=torch.double)
+    a, b = -0.5 * s * s, s  # tangent lines of z^2/2
+    perm = torch.randperm(L, generator=torch.Generator().manual_seed(0))
+    a, b = a[perm][None], b[perm][None]
+    got, hull = kg_from_lines(a.to(DEV), b.to(DEV), return_hull_size=True)
+    ref = _oracle_lines_kg(a, b)
+    assert_kg_close(got.cpu(), ref, 64 * torch.finfo(torch.double).eps * a.abs().amax(-1))
+    assert int(hull) == L
+
+
+def test_lines_kg_empty_raises():
+    from dkg_amd import kg_from_lines
+
+    with pytest.raises(ValueError, match="at least one line"):
+        kg_from_lines(torch.empty(3, 0, device=DEV), torch.empty(3, 0, device=DEV))
+
+
+# ---------------------------------------------------------------- posterior stage
+def test_cross_root_matches_dense_product():
+    from dkg_amd.gp_state import DeviceGPState
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    st = DeviceGPState(model, D)
+    om = to_oracle(model)
+    for c, o in zip(st.outputs, om.models):
+        ref_mu = (o.covar(D, o.train_x) @ o.cache()["alpha"] + o.mean_constant)
+        torch.testing.assert_close(c.disc_mean[: D.shape[0]].cpu(), ref_mu, rtol=1e-9, atol=1e-9)
+        n = o.train_x.shape[0]
+        Qd = o.covar(D, o.train_x) @ o.cache()["R"]
+        N = D.shape[0]
+        npad = (n + 15) // 16 * 16
+        Npad = (N + 15) // 16 * 16
+        F = c.disc_frag.cpu().reshape(Npad // 16, npad // 4, 4, 16)  # [t][kb][l>>4][l&15]
+        dense = F.permute(0, 3, 1, 2).reshape(Npad, npad)[:N, :n]
+        torch.testing.assert_close(dense, Qd, rtol=1e-8, atol=1e-8)
+
+
+# ---------------------------------------------------------------- end to end
+@pytest.fixture(scope="module")
+def ref_model():
+    return make_reference_test_model(use_noise=True)
+
+
+def test_reference_kat_table_full(ref_model):
+    """test_discretekg.py:50-63 through the HIP path."""
+    from dkg_amd import DiscreteKnowledgeGradient
+
+    X = torch.tensor([[[[0.5, 0.5]], [[0, 1]], [[0, 0.5]]], [[[0, 0]], [[1, 0]], [[0.5, 0]]]], dtype=torch.double)
+    acq = DiscreteKnowledgeGradient(to_state(ref_model), reference_test_discretisation(), torch.tensor(TRIO))
+    kg = acq(X)
+    torch.testing.assert_close(kg, torch.tensor([[0.0383, 0.0224, 0.0130], [0.0005, 0.0058, 0.0015]]),
+                               atol=1e-4, rtol=1e-3)
+    ref = discrete_kg_forward(ref_model, X, reference_test_discretisation(), torch.tensor(TRIO))
+    floor = rounding_floor(ref_model, X.reshape(-1, 2), reference_test_discretisation(), torch.tensor(TRIO))
+    assert_kg_close(kg, ref, floor)
+
+
+def test_reference_kat_table_single_output(ref_model):
+    """test_discretekg.py:65-79 through the HIP path."""
+    from dkg_amd import DiscreteKnowledgeGradient
+
+    X = torch.tensor([[[[0.5, 0.5]], [[0, 1]], [[0, 0.5]]], [[[0, 0]], [[1, 0]], [[0.5, 0]]]], dtype=torch.double)
+    acq = DiscreteKnowledgeGradient(to_state(ref_model), reference_test_discretisation(), torch.tensor(TRIO),
+                                    target_output_ix=0)
+    kg = acq(X)
+    torch.testing.assert_close(kg, torch.tensor([[0.0297, 0.0084, 0.0048], [0.0002, 0.0030, 0.0006]]),
+                               atol=1e-4, rtol=1e-3)
+
+
+def test_reference_kat_scalars(ref_model):
+    """test_discretekg.py:87-108: the rel-1e-6 known answers."""
+    from dkg_amd import calculate_discrete_kg as gpu_kg
+    from dkg_amd import calculate_discrete_kg_conditioning_on_single_output as gpu_kg1
+
+    D = reference_test_discretisation()
+    W = torch.tensor(TRIO)
+    x = torch.tensor([0.5, 0.5])
+    assert float(gpu_kg(to_state(ref_model), x, D, W)) == pytest.approx(0.038261974207699244, rel=1e-6)
+    assert float(gpu_kg1(to_state(ref_model), x, 0, D, W)) == pytest.approx(0.02968190595713936, rel=1e-6)
+    assert float(calculate_discrete_kg(ref_model, x, D, W)) == pytest.approx(0.038261974207699244)
+    assert float(calculate_discrete_kg_conditioning_on_single_output(ref_model, x, 0, D, W)) == pytest.approx(
+        0.02968190595713936)
+
+
+@pytest.mark.parametrize("workload", ["small", "parity6d"])
+@pytest.mark.parametrize("target", [None, 0, 1])
+def test_forward_vs_faithful_oracle(workload, target):
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS[workload])
+    X = X[:16]
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)
+    got = acq(X.unsqueeze(-2))
+    om = to_oracle(model)
+    ref = discrete_kg_forward(om, X.unsqueeze(-2), D, W, target)
+    assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
+    assert bool((got >= 0).all())
+
+
+@pytest.mark.parametrize("target", [None, 0, 1])
+def test_headline_vs_batched_oracle(target):
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["headline"])
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)
+    pairs = acq.forward_pairs(X.unsqueeze(-2)).cpu()
+    got = acq(X.unsqueeze(-2)).cpu()
+    om = to_oracle(model)
+    ref, ref_pairs = discrete_kg_batched(om, X[:48], D, W, target)
+    floor = rounding_floor(om, X[:48], D, W, target)
+    assert_kg_close(got[:48], ref, floor)
+    assert_kg_close(pairs[:48], ref_pairs, floor[:, None].expand_as(ref_pairs))
+    torch.testing.assert_close(got, pairs.mean(-1), rtol=1e-14, atol=1e-300)
+
+
+def test_forward_deterministic_and_permutation_equivariant():
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["headline"])
+    acq = DiscreteKnowledgeGradient(model, D, W)
+    k1 = acq(X.unsqueeze(-2))
+    k2 = acq(X.unsqueeze(-2))
+    assert torch.equal(k1, k2)
+    perm = torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(3))
+    k3 = acq(X[perm].unsqueeze(-2))
+    assert torch.equal(k3, k1[perm])
+    # scalarisation order does not change the mean beyond rounding
+    acq2 = DiscreteKnowledgeGradient(model, D, W.flip(0))
+    torch.testing.assert_close(acq2(X.unsqueeze(-2)), k1, rtol=1e-13, atol=1e-300)
+
+
+def test_odd_sizes_and_padding():
+    """n, N, B, S not multiples of 16, d = 3, three outputs with different n."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.model import ModelListGPState, SingleTaskGPState
+
+    g = torch.Generator().manual_seed(5)
+    outs = []
+    for i, n in enumerate([37, 50, 23]):
+        X = torch.rand(n, 3, generator=g, dtype=torch.double)
+        y = torch.sin(3 * X.sum(-1) + i) + 0.1 * torch.randn(n, generator=g, dtype=torch.double)
+        outs.append(SingleTaskGPState(X, y, [0.3, 0.5, 0.7][: 3], 1.0 + i, 1e-3, 0.1 * i,
+                                      kernel=["matern", "matern", "rbf"][i], nu=[2.5, 1.5, None][i],
+                                      y_mean=0.3 * i, y_std=1.0 + 0.5 * i))
+    model = ModelListGPState(*outs)
+    D = torch.rand(77, 3, generator=g, dtype=torch.double)
+    W = torch.rand(5, 3, generator=g, dtype=torch.double)
+    W = W / W.sum(-1, keepdim=True)
+    Xc = torch.rand(19, 3, generator=g, dtype=torch.double)
+    om = to_oracle(model)
+    for target in (None, 0, 2):
+        got = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)(Xc.unsqueeze(-2))
+        ref = discrete_kg_forward(om, Xc.unsqueeze(-2), D, W, target)
+        assert_kg_close(got, ref, rounding_floor(om, Xc, D, W, target))
+
+
+def test_matern12_single_output_and_no_weights():
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.model import ModelListGPState, SingleTaskGPState
+
+    g = torch.Generator().manual_seed(9)
+    X = torch.rand(40, 2, generator=g, dtype=torch.double)
+    y = torch.cos(4 * X[:, 0]) * X[:, 1]
+    model = ModelListGPState(SingleTaskGPState(X, y, [0.4, 0.3], 2.0, 1e-2, 0.0, kernel="matern", nu=0.5))
+    D = torch.rand(100, 2, generator=g, dtype=torch.double)
+    Xc = torch.rand(10, 1, 2, generator=g, dtype=torch.double)
+    got = DiscreteKnowledgeGradient(model, D)(Xc)
+    om = to_oracle(model)
+    ref = discrete_kg_forward(om, Xc, D, torch.tensor([[1.0]]))
+    assert_kg_close(got, ref, rounding_floor(om, Xc.squeeze(1), D, torch.tensor([[1.0]])))
+
+
+def test_lines_match_oracle_lines_headline():
+    """The KG per (candidate, scalarisation) equals the reference epigraph on oracle lines."""
+    from dkg_amd import DiscreteKnowledgeGradient, kg_from_lines
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["headline"])
+    om = to_oracle(model)
+    a, b = lines_batched(om, X[:8], D, W, None)
+    got = kg_from_lines(a.to(DEV), b.to(DEV)).cpu()
+    ref = torch.stack([torch.stack([_kg_from_lines(a[i, j], b[i, j]) for j in range(a.shape[1])])
+                       for i in range(a.shape[0])])
+    assert_kg_close(got, ref, 64 * torch.finfo(torch.double).eps * a.abs().amax(-1))
+    del DiscreteKnowledgeGradient

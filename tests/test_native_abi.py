@@ -1,0 +1,86 @@
+"""The C-ABI library loads and exports every symbol ``include/dkg.h`` declares.
+
+CPU-only: no compute entry point is called with device data here; argument
+validation paths that return before touching the GPU are exercised.
+"""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from dkg_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "dkg.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(dkg_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    assert "dkg_forward" in names and "dkg_lines_kg" in names and len(names) >= 10
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_abi_version():
+    assert _lib.load().dkg_abi_version() == _lib.ABI_VERSION
+
+
+def test_frag_elems():
+    lib = _lib.load()
+    assert lib.dkg_frag_elems(1024, 256) == 1024 * 256
+    assert lib.dkg_frag_elems(10, 10) == 16 * 16
+    assert lib.dkg_frag_elems(0, 7) == 0
+
+
+def test_struct_layout_matches_header():
+    # int32 n, int32 kernel, 5 doubles, 6 pointers
+    assert ctypes.sizeof(_lib.DkgOutput) == 4 + 4 + 5 * 8 + 6 * 8
+    assert _lib.DkgOutput.inv_lengthscale.offset == 48
+
+
+def test_validation_errors_without_device():
+    lib = _lib.load()
+    # no lines -> the reference's ValueError message (discretekg.py:466-470)
+    st = lib.dkg_lines_kg(None, None, 3, 0, None, None, None)
+    assert st == _lib.DKG_ERR_NO_LINES
+    assert b"at least one line" in lib.dkg_last_error()
+    with pytest.raises(ValueError, match="at least one line"):
+        _lib.check(st, "dkg_lines_kg")
+    # unsupported number of outputs
+    outs = (_lib.DkgOutput * 1)()
+    st = lib.dkg_forward(outs, 9, 2, None, 4, None, 1, None, 1, -1, None, None, None, 0, None)
+    assert st == _lib.DKG_ERR_UNSUPPORTED
+    # missing device state pointers -> argument error
+    outs[0].n = 4
+    outs[0].kernel = 2
+    st = lib.dkg_forward(outs, 1, 2, None, 4, None, 1, None, 1, -1, None, None, None, 0, None)
+    assert st == _lib.DKG_ERR_ARG
+    # target out of range
+    for f in ("inv_lengthscale", "train_x", "alpha", "root_frag", "disc_frag", "disc_mean"):
+        setattr(outs[0], f, 16)
+    st = lib.dkg_forward(outs, 1, 2, None, 4, None, 1, None, 1, 3, None, None, None, 0, None)
+    assert st == _lib.DKG_ERR_ARG and b"target" in lib.dkg_last_error()
+    # empty batch is a no-op
+    assert lib.dkg_forward(outs, 1, 2, 16, 4, 16, 0, 16, 1, -1, 16, None, 16, 0, None) == _lib.DKG_OK
+
+
+def test_workspace_size_grows_with_problem():
+    lib = _lib.load()
+    outs = (_lib.DkgOutput * 2)()
+    outs[0].n = outs[1].n = 256
+    small = lib.dkg_forward_workspace(outs, 2, 256, 32, 8)
+    big = lib.dkg_forward_workspace(outs, 2, 1024, 128, 16)
+    assert 0 < small < big
+    assert big >= 2 * 128 * 1024 * 8  # the covariance rows of both outputs
