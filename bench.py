@@ -111,14 +111,15 @@ def main():
     if rank == 0:
         X = X0
     acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=args.target, device=dev)
-    state = acq._state
+    plan = acq._plan_for(w.B)
     Xd = X.to(dev).contiguous()
-    Wd = W.to(dev)
+    kgs = [torch.empty(w.B, dtype=torch.double, device=dev) for _ in range(2)]
     gathered = [torch.empty(world * w.B, dtype=torch.double, device=dev) for _ in range(2)]
     works = [None, None]
 
     def step(k):
-        kg = state.forward(Xd, Wd, args.target)
+        kg = kgs[k % 2]
+        plan.forward_into(Xd, kg)
         if world > 1:
             slot = k % 2
             if works[slot] is not None:
@@ -156,7 +157,7 @@ def main():
     names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
     acc = [0.0, 0.0, 0.0]
     for _ in range(args.profile_reps):
-        _, ms = state.forward(Xd, Wd, args.target, timed=True)
+        _, ms = plan.forward(Xd, timed=True)
         acc = [a + b for a, b in zip(acc, ms)]
     avg_ms = [a / args.profile_reps for a in acc]
     model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)

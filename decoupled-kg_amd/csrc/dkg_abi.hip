@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "dkg_kernels.h"
@@ -69,6 +70,8 @@ int check_outputs(const dkg_output* outs, int m, int d) {
     const dkg_output& o = outs[i];
     if (o.n < 1) return fail(DKG_ERR_ARG, "output %d: n=%d training points", i, o.n);
     if (pad16(o.n) > 1024) return fail(DKG_ERR_UNSUPPORTED, "output %d: n=%d > 1024 training points", i, o.n);
+    if (cross_root_lds_bytes(pad16(o.n), d) > 160 * 1024)
+      return fail(DKG_ERR_UNSUPPORTED, "output %d: n=%d, d=%d exceed the cross stage's LDS budget", i, o.n, d);
     if (o.kernel < DKG_MATERN12 || o.kernel > DKG_RBF) return fail(DKG_ERR_ARG, "output %d: kernel id %d", i, o.kernel);
     if (!o.inv_lengthscale || !o.train_x || !o.alpha || !o.root_frag)
       return fail(DKG_ERR_ARG, "output %d: missing device state pointer", i);
@@ -76,96 +79,92 @@ int check_outputs(const dkg_output* outs, int m, int d) {
   return DKG_OK;
 }
 
-int forward_impl(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew, int B,
-                 const double* weights, int S, int target, double* kg, double* kg_pairs, void* workspace,
-                 size_t workspace_bytes, hipStream_t stream, float* stage_ms) {
+int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
+               int target, int max_B, void* workspace, size_t workspace_bytes, Plan* P) {
   int st = check_outputs(outs, m, d);
   if (st) return st;
-  if (B < 0 || N < 0) return fail(DKG_ERR_ARG, "negative size B=%d N=%d", B, N);
+  if (max_B < 0 || N < 0) return fail(DKG_ERR_ARG, "negative size B=%d N=%d", max_B, N);
   if (S < 1) return fail(DKG_ERR_ARG, "S=%d scalarisations", S);
   if (target < -1 || target >= m) return fail(DKG_ERR_ARG, "target_output_ix=%d out of range for %d outputs", target, m);
   if (N + 1 > 64 * 33) return fail(DKG_ERR_UNSUPPORTED, "N=%d discretisation points (supported <= %d)", N, 64 * 33 - 1);
-  if (B == 0) return DKG_OK;
-  if (!xnew || !weights || !kg || !workspace || (N > 0 && !disc)) return fail(DKG_ERR_ARG, "NULL data pointer");
+  int sw, split;
+  envelope_geometry(std::max(max_B, 1), S, &sw, &split);
+  if (envelope_lds_bytes(m, N, sw, S) > 160 * 1024)
+    return fail(DKG_ERR_UNSUPPORTED, "m=%d outputs x N=%d points exceed the envelope stage's LDS staging", m, N);
+  if (!weights || !workspace || (N > 0 && !disc)) return fail(DKG_ERR_ARG, "NULL data pointer");
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
-  const WsLayout L = layout(outs, m, N, B, S);
+  const WsLayout L = layout(outs, m, N, max_B, S);
   if (workspace_bytes < L.total)
     return fail(DKG_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, L.total);
   char* ws = static_cast<char*>(workspace);
-
-  Outputs O{};
-  int max_np = 16;
+  *P = Plan{};
+  P->m = m;
+  P->d = d;
+  P->N = N;
+  P->S = S;
+  P->target = target;
+  P->max_B = max_B;
+  P->max_np = 16;
+  P->sw = sw;
+  P->split = split;
+  P->disc = disc;
+  P->weights = weights;
   for (int i = 0; i < m; ++i) {
-    O.o[i] = outs[i];
-    max_np = std::max(max_np, pad16(outs[i].n));
+    P->o[i] = outs[i];
+    P->max_np = std::max(P->max_np, pad16(outs[i].n));
+    P->q[i] = reinterpret_cast<double*>(ws + L.q[i]);
+    P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
+    P->cov[i] = reinterpret_cast<double*>(ws + L.cov[i]);
   }
+  P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
+  P->tickets = reinterpret_cast<int*>(ws + L.tickets);
+  static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
+  static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
+  P->debug_env = denv ? std::atoi(denv) : 0;
+  P->debug_cov = dcov ? std::atoi(dcov) : 0;
+  return DKG_OK;
+}
 
+int run_forward(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* kg_pairs,
+                hipStream_t stream, float* stage_ms) {
+  if (B < 0) return fail(DKG_ERR_ARG, "negative B=%d", B);
+  if (B == 0) return DKG_OK;
+  if (B > h.max_B) return fail(DKG_ERR_ARG, "B=%d candidates > plan capacity %d", B, h.max_B);
+  if (!xnew || !kg) return fail(DKG_ERR_ARG, "NULL data pointer");
   hipEvent_t ev[4];
-  if (stage_ms) {
+  int st;
+  if (stage_ms)
     for (int k = 0; k < 4; ++k)
       if ((st = hip_check(hipEventCreate(&ev[k]), "hipEventCreate"))) return st;
-    (void)hipEventRecord(ev[0], stream);
-  }
-
-  CrossArgs ca{};
-  ca.outs = O;
-  ca.d = d;
-  ca.rows = B;
-  ca.x = xnew;
-  for (int i = 0; i < m; ++i) {
-    ca.q[i] = reinterpret_cast<double*>(ws + L.q[i]);
-    ca.mean[i] = reinterpret_cast<double*>(ws + L.mux[i]);
-  }
-  ca.tickets = reinterpret_cast<int*>(ws + L.tickets);
-  ca.n_tickets = B;
-  if ((st = hip_check(launch_cross_root(ca, m, max_np, stream), "cross_root_kernel"))) return st;
-  if (stage_ms) (void)hipEventRecord(ev[1], stream);
-
-  CovArgs cv{};
-  cv.outs = O;
-  cv.d = d;
-  cv.N = N;
-  cv.B = B;
-  cv.xnew = xnew;
-  cv.disc = disc;
-  for (int i = 0; i < m; ++i) {
-    cv.q[i] = ca.q[i];
-    cv.cov[i] = reinterpret_cast<double*>(ws + L.cov[i]);
-  }
-  if (N > 0)
-    if ((st = hip_check(launch_posterior_cov(cv, m, stream), "posterior_cov_kernel"))) return st;
-  if (stage_ms) (void)hipEventRecord(ev[2], stream);
-
-  EnvArgs ea{};
-  ea.outs = O;
-  ea.m = m;
-  ea.N = N;
-  ea.S = S;
-  ea.B = B;
-  ea.target = target;
-  ea.weights = weights;
-  for (int i = 0; i < m; ++i) {
-    ea.q[i] = ca.q[i];
-    ea.mux[i] = ca.mean[i];
-    ea.cov[i] = cv.cov[i];
-  }
-  ea.kg = kg;
-  ea.pairs_out = kg_pairs;
-  ea.wg_part = reinterpret_cast<double*>(ws + L.wg_part);
-  ea.tickets = ca.tickets;
-  int sw, split;
-  envelope_geometry(B, S, &sw, &split);
-  if ((st = hip_check(launch_envelope(ea, sw, split, stream), "envelope_kernel"))) return st;
-
+  if ((st = hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, stream, stage_ms ? ev : nullptr), "forward")))
+    return st;
   if (stage_ms) {
-    (void)hipEventRecord(ev[3], stream);
     if ((st = hip_check(hipEventSynchronize(ev[3]), "hipEventSynchronize"))) return st;
     for (int k = 0; k < 3; ++k) (void)hipEventElapsedTime(&stage_ms[k], ev[k], ev[k + 1]);
     for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
   }
   return DKG_OK;
+}
+
+size_t plan_slot_bytes() { return align256(sizeof(Plan)); }
+
+// One-shot path: plan built on the host per call, its device copy placed in
+// the workspace tail (one small host-to-device copy per call).
+int forward_oneshot(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew, int B,
+                    const double* weights, int S, int target, double* kg, double* kg_pairs, void* workspace,
+                    size_t workspace_bytes, hipStream_t stream, float* stage_ms) {
+  if (B == 0) return check_outputs(outs, m, d);
+  const size_t slot = plan_slot_bytes() + 256;
+  const size_t avail = workspace_bytes > slot ? workspace_bytes - slot : 0;
+  thread_local Plan h;
+  int st = build_plan(outs, m, d, disc, N, weights, S, target, B, workspace, avail, &h);
+  if (st) return st;
+  Plan* dev = reinterpret_cast<Plan*>((reinterpret_cast<uintptr_t>(workspace) + avail + 255) & ~(uintptr_t)255);
+  if ((st = hip_check(hipMemcpyAsync(dev, &h, sizeof(Plan), hipMemcpyHostToDevice, stream), "hipMemcpyAsync")))
+    return st;
+  return run_forward(h, dev, xnew, B, kg, kg_pairs, stream, stage_ms);
 }
 
 }  // namespace
@@ -200,33 +199,65 @@ int dkg_cross_root(const dkg_output* o, int d, const double* x, int rows, double
   if (rows < 0 || !q_frag || (rows > 0 && !x)) return fail(DKG_ERR_ARG, "bad arguments");
   if (rows == 0) return DKG_OK;
   CrossArgs ca{};
-  ca.outs.o[0] = *o;
+  ca.o = *o;
   ca.d = d;
   ca.rows = rows;
   ca.x = x;
-  ca.q[0] = q_frag;
-  ca.mean[0] = mean;
-  return hip_check(launch_cross_root(ca, 1, pad16(o->n), (hipStream_t)stream), "cross_root_kernel");
+  ca.q = q_frag;
+  ca.mean = mean;
+  return hip_check(launch_cross_root(ca, (hipStream_t)stream), "cross_root_kernel");
 }
 
 size_t dkg_forward_workspace(const dkg_output* outs, int m, int N, int B, int S) {
   if (!outs || m < 1 || m > DKG_MAX_OUTPUTS) return 0;
-  return layout(outs, m, N, B, S).total;
+  return layout(outs, m, N, B, S).total + plan_slot_bytes() + 256;
 }
 
 int dkg_forward(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew, int B,
                 const double* weights, int S, int target, double* kg, double* kg_pairs, void* workspace,
                 size_t workspace_bytes, void* stream) {
-  return forward_impl(outs, m, d, disc, N, xnew, B, weights, S, target, kg, kg_pairs, workspace,
-                      workspace_bytes, (hipStream_t)stream, nullptr);
+  return forward_oneshot(outs, m, d, disc, N, xnew, B, weights, S, target, kg, kg_pairs, workspace, workspace_bytes,
+                         (hipStream_t)stream, nullptr);
 }
 
 int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew,
                       int B, const double* weights, int S, int target, double* kg, double* kg_pairs,
                       void* workspace, size_t workspace_bytes, void* stream, float* stage_ms) {
   if (!stage_ms) return fail(DKG_ERR_ARG, "stage_ms is NULL");
-  return forward_impl(outs, m, d, disc, N, xnew, B, weights, S, target, kg, kg_pairs, workspace,
-                      workspace_bytes, (hipStream_t)stream, stage_ms);
+  return forward_oneshot(outs, m, d, disc, N, xnew, B, weights, S, target, kg, kg_pairs, workspace, workspace_bytes,
+                         (hipStream_t)stream, stage_ms);
+}
+
+size_t dkg_plan_bytes(void) { return sizeof(Plan); }
+
+size_t dkg_plan_workspace(const dkg_output* outs, int m, int N, int max_B, int S) {
+  if (!outs || m < 1 || m > DKG_MAX_OUTPUTS) return 0;
+  return layout(outs, m, N, max_B, S).total;
+}
+
+int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
+                  int target, int max_B, void* workspace, size_t workspace_bytes, void* host_plan, void* dev_plan,
+                  void* stream) {
+  if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  Plan* h = static_cast<Plan*>(host_plan);
+  int st = build_plan(outs, m, d, disc, N, weights, S, target, max_B, workspace, workspace_bytes, h);
+  if (st) return st;
+  return hip_check(hipMemcpyAsync(dev_plan, h, sizeof(Plan), hipMemcpyHostToDevice, (hipStream_t)stream),
+                   "hipMemcpyAsync");
+}
+
+int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                     double* kg_pairs, void* stream) {
+  if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  return run_forward(*static_cast<const Plan*>(host_plan), static_cast<const Plan*>(dev_plan), xnew, B, kg, kg_pairs,
+                     (hipStream_t)stream, nullptr);
+}
+
+int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                           double* kg_pairs, void* stream, float* stage_ms) {
+  if (!host_plan || !dev_plan || !stage_ms) return fail(DKG_ERR_ARG, "NULL pointer");
+  return run_forward(*static_cast<const Plan*>(host_plan), static_cast<const Plan*>(dev_plan), xnew, B, kg, kg_pairs,
+                     (hipStream_t)stream, stage_ms);
 }
 
 int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,
@@ -238,6 +269,15 @@ int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, d
   if (L > 64 * 33) return fail(DKG_ERR_UNSUPPORTED, "L=%d lines per set (supported <= %d)", L, 64 * 33);
   if (!intercepts || !slopes || !kg) return fail(DKG_ERR_ARG, "NULL pointer");
   return hip_check(launch_lines_kg(intercepts, slopes, P, L, kg, n_hull, (hipStream_t)stream), "lines_kg_kernel");
+}
+
+int dkg_debug_read_stamps(unsigned long long* host, int n) {
+  return hip_check(read_stamps(host, n), "hipMemcpyFromSymbol");
+}
+
+int dkg_debug_wave_ops(const double* in, double* out, void* stream) {
+  if (!in || !out) return fail(DKG_ERR_ARG, "NULL pointer");
+  return hip_check(launch_debug_wave(in, out, (hipStream_t)stream), "debug_wave_kernel");
 }
 
 int dkg_debug_mfma_f64(const double* a, const double* b, double* c, void* stream) {

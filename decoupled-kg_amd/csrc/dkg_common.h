@@ -65,17 +65,56 @@ __device__ __forceinline__ double scaled_r2_reg(const double (&xa)[DKG_MAX_DIM],
   return acc;
 }
 
+// ---------------------------------------------------------------------------
+// Wave butterflies: DPP within 16-lane rows (xor 1, xor 2 via quad_perm;
+// row_half_mirror; row_mirror), then two cross-row exchanges.  Each step
+// hands every lane the value of a partner lane in the other half of its
+// current group; with a commutative combine all lanes end with the same result.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Returns the partner value of `v` for butterfly step `s` (0..5).
+// Cross-row steps (xor 16, xor 32) use ds_bpermute.  The gfx950
+// v_permlane16_swap / v_permlane32_swap builtins pass an isolated self-test
+// (tests: test_wave_butterfly_primitives) but returned stale partner values
+// inside the envelope walk loop (ROCm 7.2 hipcc; DESIGN.md "Known issues"),
+// so they are not used.
+template <int STEP>
+__device__ __forceinline__ double partner_f64(double v) {
+  if constexpr (STEP == 0) return dpp_f64<0xB1>(v);        // quad_perm [1,0,3,2]
+  else if constexpr (STEP == 1) return dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  else if constexpr (STEP == 2) return dpp_f64<0x141>(v);  // row_half_mirror
+  else if constexpr (STEP == 3) return dpp_f64<0x140>(v);  // row_mirror
+  else return __shfl_xor(v, STEP == 4 ? 16 : 32);
+}
+
+#define DKG_BUTTERFLY(...)                         \
+  {                                                \
+    { constexpr int S_ = 0; __VA_ARGS__ }          \
+    { constexpr int S_ = 1; __VA_ARGS__ }          \
+    { constexpr int S_ = 2; __VA_ARGS__ }          \
+    { constexpr int S_ = 3; __VA_ARGS__ }          \
+    { constexpr int S_ = 4; __VA_ARGS__ }          \
+    { constexpr int S_ = 5; __VA_ARGS__ }          \
+  }
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  DKG_BUTTERFLY({ v = v + partner_f64<S_>(v); })
   return v;
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  DKG_BUTTERFLY({ v = fmax(v, partner_f64<S_>(v)); })
   return v;
 }
+
+// A condition every lane agrees on, made visibly wave-uniform (scalar branch,
+// full EXEC) so cross-lane operations inside the branch see every lane.
+__device__ __forceinline__ bool uniform(bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; }
 
 __device__ __forceinline__ int lanes_below(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));

@@ -5,50 +5,50 @@
 
 namespace dkg {
 
+// Everything a forward needs besides the candidates, resident in device memory
+// (written once per (model, discretisation, weights) by dkg_plan_init): the
+// kernels take a pointer to it, so each launch carries ~40 bytes of arguments
+// instead of a ~1 KiB by-value block (measured ~1.5 us of launch cost).
+struct Plan {
+  dkg_output o[DKG_MAX_OUTPUTS];
+  int32_t m, d, N, S, target;       // target < 0: all outputs observed
+  int32_t max_B, max_np;            // workspace sized for max_B candidates; max n_pad over outputs
+  int32_t sw, split;                // envelope geometry: waves per workgroup, workgroups per candidate
+  int32_t debug_env, debug_cov;     // ablation switches (0 in production)
+  int32_t pad_;
+  const double* disc;               // [N x d]
+  const double* weights;            // [S x m]
+  double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
+  double* mux[DKG_MAX_OUTPUTS];     // posterior mean at the candidates per output (workspace)
+  double* cov[DKG_MAX_OUTPUTS];     // [B x N] posterior covariance rows per output (workspace)
+  double* wg_part;                  // [B x split] partial sums (split > 2 only)
+  int* tickets;                     // [B] arrival counters (split > 2 only)
+};
+
+// By-value arguments of the state-preparation use of the cross stage.
 struct CrossArgs {
-  Outputs outs;
-  int d;
-  int rows;
-  const double* x;                       // [rows x d]
-  double* q[DKG_MAX_OUTPUTS];            // fragment-packed Q per output
-  double* mean[DKG_MAX_OUTPUTS];         // [pad16(rows)] per output (nullable)
-  int* tickets;                          // zeroed by one workgroup (nullable)
-  int n_tickets;
-};
-
-struct CovArgs {
-  Outputs outs;
-  int d, N, B;
-  const double* xnew;                    // [B x d]
-  const double* disc;                    // [N x d]
-  const double* q[DKG_MAX_OUTPUTS];      // fragment-packed Q_x per output
-  double* cov[DKG_MAX_OUTPUTS];          // [B x N] per output
-};
-
-struct EnvArgs {
-  Outputs outs;
-  int m, N, S, B, target;
-  const double* weights;                 // [S x m]
-  const double* q[DKG_MAX_OUTPUTS];
-  const double* mux[DKG_MAX_OUTPUTS];
-  const double* cov[DKG_MAX_OUTPUTS];
-  double* kg;                            // [B]
-  double* pairs_out;                     // [B x S] nullable
-  double* wg_part;                       // [B x SPLIT]
-  int* tickets;                          // [B], zero on entry
+  dkg_output o;
+  int d, rows;
+  const double* x;  // [rows x d]
+  double* q;        // fragment-packed Q
+  double* mean;     // [pad16(rows)] (nullable)
 };
 
 hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, int n1, const double* x2, int n2,
                                 double diag_add, double* out, hipStream_t s);
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
-hipError_t launch_cross_root(const CrossArgs& a, int m, int max_np, hipStream_t s);
-hipError_t launch_posterior_cov(const CovArgs& a, int m, hipStream_t s);
-hipError_t launch_envelope(const EnvArgs& a, int waves_per_wg, int split, hipStream_t s);
+hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
+hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
+                          hipStream_t s, hipEvent_t* ev);
 hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s);
+hipError_t read_stamps(unsigned long long* host, int n);
+hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s);
 hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStream_t s);
 
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and
 // workgroups per candidate.
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split);
+size_t envelope_lds_bytes(int m, int N, int waves, int S);
+size_t cross_root_lds_bytes(int np, int d);
 
 }  // namespace dkg

@@ -45,68 +45,85 @@ __global__ void pack_root_kernel(const double* __restrict__ r, int n, double* __
 // The pair is (p, T-1-p) of 16-column tiles of Q = K_x R; R upper triangular
 // means tile tj only needs k-blocks kb < 4(tj+1), so pairing the shortest
 // with the longest tile balances the MFMA count across workgroups.  The
-// K(x, X) tile is evaluated once into LDS in B-operand order and the k range
-// is split over the 8 waves (split-K), partials reduced in LDS in fixed order.
+// training inputs are staged in LDS, the K(x, X) tile is evaluated once into
+// LDS in B-operand order, and the k range is split over the 8 waves
+// (split-K) with every operand of a wave's chunk loaded before its MFMAs;
+// partials are reduced in LDS in fixed wave order (deterministic).
 constexpr int CR_WAVES = 8;
+constexpr int CR_U = 8;  // k-blocks per load batch
 
-__global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs args) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int ti = blockIdx.x;
-  const int p = blockIdx.y;
-  const int oi = blockIdx.z;
-  const dkg_output& o = args.outs.o[oi];
-  const int d = args.d;
-  const int rows = args.rows;
+__device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
+                                                double* __restrict__ qout, double* __restrict__ mout, int ti, int p,
+                                                double* smem) {
   const int n = o.n;
   const int np = pad16(n);
   const int T = np / 16;
   const int KB = np / 4;
   const int P = (T + 1) / 2;
   if (p >= P) return;
-  const int tA = p, tB = T - 1 - p;       // tA <= tB
+  const int tA = p, tB = T - 1 - p;                  // tA <= tB
   const int kbA = 4 * (tA + 1), kbB = 4 * (tB + 1);  // k-block extents (kbB >= kbA)
+  const int ncol = min(n, 4 * kbB);                  // training columns this pair needs
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  double* kb_lds = smem;                                   // [kbB][64]
-  double* part = smem + (size_t)KB * 64;                   // [CR_WAVES][8][64]
-  double* mred = part + CR_WAVES * 8 * 64;                 // [CR_WAVES][16]
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* kb_lds = smem;                         // [KB][64]
+  double* part = kb_lds + (size_t)KB * 64;       // [CR_WAVES][8][64]
+  double* mred = part + CR_WAVES * 8 * 64;       // [CR_WAVES][16]
+  double* xs = mred + CR_WAVES * 16;             // [np][d] staged training inputs
+  double* als = xs + (size_t)np * d;             // [np] alpha
 
-  // ---- fill K(x_row, X_col) for col < 4*kbB, in B-operand order.
+  const bool want_mean = (mout != nullptr) && (p == 0);  // p == 0 covers every column
+  for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e];
+  if (want_mean)
+    for (int e = tid; e < ncol; e += CR_WAVES * WAVE) als[e] = o.alpha[e];
   const int row = ti * 16 + (lane & 15);
   const bool rv = row < rows;
   double xr[DKG_MAX_DIM];
 #pragma unroll
-  for (int k = 0; k < DKG_MAX_DIM; ++k) xr[k] = (rv && k < d) ? args.x[(size_t)row * d + k] : 0.0;
-  const bool want_mean = (args.mean[oi] != nullptr) && (p == 0);  // p == 0 covers every column
+  for (int k = 0; k < DKG_MAX_DIM; ++k) xr[k] = (rv && k < d) ? x[(size_t)row * d + k] : 0.0;
+  __syncthreads();
+
+  // ---- fill K(x_row, X_col), col < 4*kbB, in B-operand order (zero outside)
   double mpart = 0.0;
   for (int e = tid; e < kbB * 64; e += CR_WAVES * WAVE) {
     const int col = 4 * (e >> 6) + (lane >> 4);
     double v = 0.0;
     if (rv && col < n) {
-      v = o.outputscale *
-          kernel_profile(o.kernel, scaled_r2_reg(xr, o.train_x + (size_t)col * d, o.inv_lengthscale, d));
-      if (want_mean) mpart = fma(v, o.alpha[col], mpart);
+      v = o.outputscale * kernel_profile(o.kernel, scaled_r2_reg(xr, xs + (size_t)col * d, o.inv_lengthscale, d));
+      if (want_mean) mpart = fma(v, als[col], mpart);
     }
     kb_lds[e] = v;
   }
   __syncthreads();
 
-  // ---- split-K MFMA over the pair.
+  // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
   const double* rfA = o.root_frag + (size_t)tA * KB * 64 + lane;
   const double* rfB = o.root_frag + (size_t)tB * KB * 64 + lane;
   const int chunk = (kbB + CR_WAVES - 1) / CR_WAVES;
   const int k0 = wave * chunk;
   const int k1 = min(kbB, k0 + chunk);
-  d4 accA = {0.0, 0.0, 0.0, 0.0};
-  d4 accB = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-  for (int kb = k0; kb < k1; ++kb) {
-    const double bop = kb_lds[kb * 64 + lane];
-    accB = mfma_f64(rfB[(size_t)kb * 64], bop, accB);
-    if (kb < kbA && tA != tB) accA = mfma_f64(rfA[(size_t)kb * 64], bop, accA);
+  d4 accA2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  d4 accB2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  const bool pairA = tA != tB;
+  for (int base = k0; base < k1; base += CR_U) {
+    double ra[CR_U], rb[CR_U], bo[CR_U];
+#pragma unroll
+    for (int u = 0; u < CR_U; ++u) {
+      const int kb = min(base + u, kbB - 1);
+      rb[u] = rfB[(size_t)kb * 64];
+      ra[u] = rfA[(size_t)min(kb, kbA - 1) * 64];
+      bo[u] = (base + u < k1) ? kb_lds[kb * 64 + lane] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < CR_U; ++u) {
+      accB2[u & 1] = mfma_f64(rb[u], bo[u], accB2[u & 1]);
+      if (pairA && base + u < kbA) accA2[u & 1] = mfma_f64(ra[u], bo[u], accA2[u & 1]);
+    }
   }
+  const d4 accA = accA2[0] + accA2[1];
+  const d4 accB = accB2[0] + accB2[1];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     part[(wave * 8 + r) * 64 + lane] = accA[r];
@@ -114,8 +131,8 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a
   }
   // mean partials: lanes l, l^16, l^32, l^48 share a row.
   if (want_mean) {
-    mpart += __shfl_xor(mpart, 16);
-    mpart += __shfl_xor(mpart, 32);
+    mpart += partner_f64<4>(mpart);
+    mpart += partner_f64<5>(mpart);
     if (lane < 16) mred[wave * 16 + lane] = mpart;
   }
   __syncthreads();
@@ -124,81 +141,126 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a
   {
     const int tsel = wave >> 2;  // 0 -> tA, 1 -> tB
     const int r = wave & 3;
-    const bool active = (tsel == 1) || (tA != tB);
-    if (active) {
+    if (tsel == 1 || pairA) {
       double s = 0.0;
+#pragma unroll
       for (int w = 0; w < CR_WAVES; ++w) s += part[(w * 8 + tsel * 4 + r) * 64 + lane];
       const int tj = tsel ? tB : tA;
       // D = R^T K^T: lane holds Q[16ti + (l&15)][16tj + 4r + (l>>4)] = q_frag[ti][4tj + r][l]
-      args.q[oi][((size_t)ti * KB + 4 * tj + r) * 64 + lane] = s;
+      qout[((size_t)ti * KB + 4 * tj + r) * 64 + lane] = s;
     }
   }
   if (want_mean && tid < 16) {
     double s = 0.0;
+#pragma unroll
     for (int w = 0; w < CR_WAVES; ++w) s += mred[w * 16 + tid];
     const int rr = ti * 16 + tid;
-    args.mean[oi][rr] = (rr < rows) ? o.mean_constant + s : 0.0;
-  }
-  if (args.tickets != nullptr && ti == 0 && p == 0 && oi == 0) {
-    for (int i = tid; i < args.n_tickets; i += blockDim.x) args.tickets[i] = 0;
+    mout[rr] = (rr < rows) ? o.mean_constant + s : 0.0;
   }
 }
 
-size_t cross_root_lds_bytes(int np) { return ((size_t)(np / 4) * 64 + CR_WAVES * 8 * 64 + CR_WAVES * 16) * 8; }
+__global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  cross_root_impl(a.o, a.d, a.x, a.rows, a.q, a.mean, blockIdx.x, blockIdx.y, smem);
+}
+
+// Forward: grid (B tiles, pairs, outputs); workgroup (0,0,0) also clears the
+// KG accumulators (and arrival tickets) the envelope stage adds into.
+__global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const Plan* __restrict__ P,
+                                                                          const double* __restrict__ xnew, int B,
+                                                                          double* __restrict__ kg) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int oi = blockIdx.z;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && oi == 0) {
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+      kg[i] = 0.0;
+      if (P->split > 2) P->tickets[i] = 0;
+    }
+  }
+  cross_root_impl(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem);
+}
+
+size_t cross_root_lds_bytes(int np, int d) {
+  return ((size_t)(np / 4) * 64 + CR_WAVES * 8 * 64 + CR_WAVES * 16 + (size_t)np * d + np) * sizeof(double);
+}
 
 // ---------------------------------------------------------------------------
 // posterior_cov_kernel: cov[b][k] = s k(x_b, D_k) - sum_l Q[b][l] Q_D[k][l]
 // One workgroup per 16x16 output tile (ti candidates x tk points) per output;
-// the 4 waves split the n_pad/4 k-blocks, operands stream straight from the
-// fragment-packed arrays (one coalesced 512-byte load per operand per MFMA),
-// partials are reduced in LDS in fixed wave order.
+// the 4 waves split the n_pad/4 k-blocks; each wave issues the loads of a
+// whole batch of PC_U k-blocks (2 x 512-byte coalesced fragment loads per
+// k-block) before its MFMAs, so the L2 latency is paid once per batch.
+// Partials are reduced in LDS in fixed wave order.
 constexpr int PC_WAVES = 4;
+constexpr int PC_U = 16;
 
-__global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(CovArgs args) {
+__global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
+                                                                         const double* __restrict__ xnew, int B) {
   __shared__ __attribute__((aligned(16))) double part[PC_WAVES * 4 * 64];
   const int tk = blockIdx.x;
   const int ti = blockIdx.y;
   const int oi = blockIdx.z;
-  const dkg_output& o = args.outs.o[oi];
-  const int N = args.N;
+  const dkg_output& o = P->o[oi];
+  const int N = P->N;
+  const int dbg = P->debug_cov;
   if (tk * 16 >= N) return;
-  const int np = pad16(o.n);
-  const int KB = np / 4;
+  const int KB = pad16(o.n) / 4;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
   const int chunk = (KB + PC_WAVES - 1) / PC_WAVES;
   const int k0 = wave * chunk;
   const int k1 = min(KB, k0 + chunk);
-  const double* qa = args.q[oi] + (size_t)ti * KB * 64 + lane;
+  const double* qa = P->q[oi] + (size_t)ti * KB * 64 + lane;
   const double* qd = o.disc_frag + (size_t)tk * KB * 64 + lane;
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-  for (int kb = k0; kb < k1; ++kb) acc = mfma_f64(qa[(size_t)kb * 64], qd[(size_t)kb * 64], acc);
+  // four independent accumulation chains (k-block mod 4): the f64 MFMA
+  // dependent-issue latency is hidden by the other chains
+  d4 acc[4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  for (int base = k0; base < k1; base += PC_U) {
+    double ra[PC_U], rb[PC_U];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) part[(wave * 4 + r) * 64 + lane] = acc[r];
+    for (int u = 0; u < PC_U; ++u) {
+      const int kb = min(base + u, KB - 1);
+      if (dbg & 1) {
+        ra[u] = 1.0 + kb;
+        rb[u] = 0.5;
+      } else {
+        ra[u] = qa[(size_t)kb * 64];
+        rb[u] = (base + u < k1) ? qd[(size_t)kb * 64] : 0.0;
+      }
+    }
+    if (dbg & 2) {
+#pragma unroll
+      for (int u = 0; u < PC_U; ++u) acc[0][u & 3] += ra[u] * rb[u];
+      continue;
+    }
+#pragma unroll
+    for (int u = 0; u < PC_U; ++u) acc[u & 3] = mfma_f64(ra[u], rb[u], acc[u & 3]);
+  }
+  const d4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  // epilogue operands (row b, column k of register r = wave) fetched while partials land
+  const int b = ti * 16 + (lane >> 4) + 4 * wave;
+  const int k = tk * 16 + (lane & 15);
+  const int d = P->d;
+  const double* xb = xnew + (size_t)min(b, B - 1) * d;
+  const double* xk = P->disc + (size_t)min(k, N - 1) * d;
+  const double r2 = scaled_r2(xb, xk, o.inv_lengthscale, d);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[(wave * 4 + r) * 64 + lane] = accs[r];
   __syncthreads();
 
-  // wave w finalises register r = w: row b = 16ti + (l>>4) + 4w, col k = 16tk + (l&15)
-  const int r = wave;
   double s = 0.0;
 #pragma unroll
-  for (int w = 0; w < PC_WAVES; ++w) s += part[(w * 4 + r) * 64 + lane];
-  const int b = ti * 16 + (lane >> 4) + 4 * r;
-  const int k = tk * 16 + (lane & 15);
-  if (b < args.B && k < N) {
-    const int d = args.d;
-    const double kv = o.outputscale * kernel_profile(o.kernel, scaled_r2(args.xnew + (size_t)b * d,
-                                                                          args.disc + (size_t)k * d,
-                                                                          o.inv_lengthscale, d));
-    args.cov[oi][(size_t)b * N + k] = kv - s;
-  }
+  for (int w = 0; w < PC_WAVES; ++w) s += part[(w * 4 + wave) * 64 + lane];
+  if (b < B && k < N)
+    P->cov[oi][(size_t)b * N + k] = ((dbg & 4) ? r2 : o.outputscale * kernel_profile(o.kernel, r2)) - s;
 }
 
 // ---------------------------------------------------------------------------
-// envelope_kernel: one wave per (candidate b, scalarisation j).
+// Envelope stage.
 //
-// Lines k = 0..N (k = 0 is the candidate itself, discretekg.py:182-183):
+// Lines k = 0..N for candidate b and weight vector w_j (k = 0 is the candidate
+// itself, discretekg.py:182-183):
 //   a_k = sum_i w_i (sd_i mu_i(z_k) + ym_i)                   (scalarised mean)
 //   b_k = sum_i beta_i sd_i^2 cov_i(x_b, z_k)                 (slope of the fantasy z)
 // full:    beta_i = w_i^2 / sqrt(sum_i w_i^2 sd_i^2 (v_i + noise_i))   (:201-223)
@@ -209,220 +271,425 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(CovArgs 
 // c_e = (a_P - a_Q) / (b_Q - b_P):
 //   KG_j = sum_{e left of T} (b_Q - b_P) psi(-c_e) + sum_{e right of T} (b_Q - b_P) psi(c_e)
 // (every term >= 0: no cancellation, unlike E - max a of the reference :233).
-// The hull: extremes L (min b), R (max b), T by wave reductions; lines above
-// the chords L-T / T-R survive into an LDS list; gift-wrapping from L over the
-// survivors (argmin of the next intersection, the reference's walk :382-401).
-constexpr int ENV_CAP = 128;  // survivor list per wave (overflow -> scan all lines)
+//
+// Per wave: extremes L (min b), R (max b), T (max a) by register butterflies;
+// the lines strictly above the chords L-T / T-R survive into an LDS list;
+// gift wrapping from L over the survivors (next vertex = argmin of the next
+// intersection, the reference's walk :382-401, compared by cross
+// multiplication); the hull edges are collected one per lane and psi is
+// evaluated for all of them at once.
+constexpr int ENV_CAP = 128;  // survivor list per wave (overflow -> walk all lines)
 
-struct Key3 {
-  double c, b, a;
-};
+// Gift wrap over all register lines (fallback when the survivor list
+// overflows ENV_CAP): next vertex = argmin of the next intersection, found by
+// a wave butterfly per hull step.
+template <int MAXL>
+__device__ __forceinline__ double envelope_walk(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
+                                             double bL, double aL, double bR, double bT, int* nhull) {
+  double bc = bL, ac = aL, kg = 0.0;
+  int h = 1;
+  for (int guard = 0; guard <= nl && uniform(bc < bR); ++guard) {
+    double bn = INFINITY, bd = 1.0, bbest = -INFINITY, abest = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const double bb = lb[t], a = la[t];
+      if (lane + 64 * t < nl && bb > bc) {
+        const double num = ac - a, den = bb - bc;
+        const double lhs = num * bd, rhs = bn * den;
+        if (bbest == -INFINITY || lhs < rhs || (lhs == rhs && bb > bbest)) { bn = num; bd = den; bbest = bb; abest = a; }
+      }
+    }
+    DKG_BUTTERFLY({
+      const double on = partner_f64<S_>(bn), od = partner_f64<S_>(bd);
+      const double ob = partner_f64<S_>(bbest), oa = partner_f64<S_>(abest);
+      bool take;
+      if (ob == -INFINITY) take = false;
+      else if (bbest == -INFINITY) take = true;
+      else {
+        const double lhs = on * bd, rhs = bn * od;
+        take = lhs < rhs || (lhs == rhs && (ob > bbest || (ob == bbest && oa > abest)));
+      }
+      if (take) { bn = on; bd = od; bbest = ob; abest = oa; }
+    })
+    if (!uniform(bbest > bc)) break;
+    const double c = bn / bd;
+    kg += (bbest - bc) * psi((bbest <= bT) ? -c : c);
+    bc = bbest;
+    ac = abest;
+    ++h;
+  }
+  if (nhull) *nhull = h;
+  return kg;
+}
 
+// KG of one set of lines held MAXL per lane (line k in lane k % 64, slot k / 64).
 template <int MAXL>
 __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
                                               double* sb, double* sa, int* nhull) {
-  // ---- extremes: T = argmax a; L = min b (tie max a); R = max b (tie max a); max |b|
-  double aT = -INFINITY, bT = 0.0;
-  double bL = INFINITY, aL = -INFINITY;
-  double bR = -INFINITY, aR = -INFINITY;
-  double babs = 0.0;
+  // ---- extremes by value, then exact tie passes (exec-masked, rarely taken):
+  // L = min b (tie: max a), R = max b (tie: max a), T = max a (tie: min b).
+  // (slots beyond nl hold padding lines: a = -inf, b = a real slope)
+  double bmin = INFINITY, bmax = -INFINITY, amax = -INFINITY;
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
-    if (lane + 64 * t < nl) {
-      const double a = la[t], bb = lb[t];
-      if (a > aT) { aT = a; bT = bb; }
-      if (bb < bL || (bb == bL && a > aL)) { bL = bb; aL = a; }
-      if (bb > bR || (bb == bR && a > aR)) { bR = bb; aR = a; }
-      babs = fmax(babs, fabs(bb));
-    }
+    bmin = fmin(bmin, lb[t]);
+    bmax = fmax(bmax, lb[t]);
+    amax = fmax(amax, la[t]);
   }
+  DKG_BUTTERFLY({
+    bmin = fmin(bmin, partner_f64<S_>(bmin));
+    bmax = fmax(bmax, partner_f64<S_>(bmax));
+    amax = fmax(amax, partner_f64<S_>(amax));
+  })
+  // short-circuit of discretekg.py:363-367 (all |b| < 1e-9), and the
+  // single-slope case (one hull vertex, E = max a): KG = 0.
+  if (!uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax)) {
+    if (nhull) *nhull = 1;
+    return 0.0;
+  }
+  double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double oaT = __shfl_xor(aT, off), obT = __shfl_xor(bT, off);
-    // tie on a: keep the smaller b so every lane agrees (deterministic)
-    if (oaT > aT || (oaT == aT && obT < bT)) { aT = oaT; bT = obT; }
-    const double obL = __shfl_xor(bL, off), oaL = __shfl_xor(aL, off);
-    if (obL < bL || (obL == bL && oaL > aL)) { bL = obL; aL = oaL; }
-    const double obR = __shfl_xor(bR, off), oaR = __shfl_xor(aR, off);
-    if (obR > bR || (obR == bR && oaR > aR)) { bR = obR; aR = oaR; }
-    babs = fmax(babs, __shfl_xor(babs, off));
+  for (int t = 0; t < MAXL; ++t) {
+    aL = fmax(aL, (lb[t] == bmin) ? la[t] : -INFINITY);
+    aR = fmax(aR, (lb[t] == bmax) ? la[t] : -INFINITY);
+    bT = fmin(bT, (la[t] == amax) ? lb[t] : INFINITY);
   }
+  DKG_BUTTERFLY({
+    aL = fmax(aL, partner_f64<S_>(aL));
+    aR = fmax(aR, partner_f64<S_>(aR));
+    bT = fmin(bT, partner_f64<S_>(bT));
+  })
+  const double bL = bmin, bR = bmax, aT = amax;
 
-  double kgj = 0.0;
-  int hull = 1;
-  // short-circuit of discretekg.py:363-367 (all slopes ~ 0), and the
-  // single-slope case: one hull vertex, E = max a, KG = 0.
-  if (babs >= 1e-9 && bL < bR) {
-    // ---- survivors strictly above the chords L-T and T-R
-    int cnt = 0;
+  // ---- survivors: lines strictly above the chords L-T (b < bT) or T-R (b > bT)
+  //      h = (a - a0)(b1 - b0) - (a1 - a0)(b - b0) > 0, as a*db - b*da > a0*db - b0*da
+  const double db1 = bT - bL, da1 = aT - aL, k1 = aL * db1 - bL * da1;
+  const double db2 = bR - bT, da2 = aR - aT, k2 = aT * db2 - bT * da2;
+  int cnt = 0;
 #pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      bool s = false;
-      const double a = la[t], bb = lb[t];
-      if (lane + 64 * t < nl) {
-        if (bb < bT) s = (bT > bL) && ((a - aL) * (bT - bL) - (aT - aL) * (bb - bL) > 0.0);
-        else if (bb > bT) s = (bR > bT) && ((a - aT) * (bR - bT) - (aR - aT) * (bb - bT) > 0.0);
-      }
-      const uint64_t mask = __ballot(s);
-      if (s) {
-        const int pos = cnt + lanes_below(mask);
-        if (pos < ENV_CAP) { sb[pos] = bb; sa[pos] = a; }
-      }
-      cnt += __popcll(mask);
+  for (int t = 0; t < MAXL; ++t) {
+    const double a = la[t], bb = lb[t];
+    const bool left = bb < bT;
+    const double db = left ? db1 : db2, da = left ? da1 : da2, kk = left ? k1 : k2;
+    const bool s = bb != bT && db > 0.0 && fma(a, db, -bb * da) > kk;
+    const uint64_t mask = __ballot(s);
+    if (s) {
+      const int pos = cnt + lanes_below(mask);
+      if (pos < ENV_CAP) { sb[pos] = bb; sa[pos] = a; }
     }
-    const bool overflow = cnt + 2 > ENV_CAP;
-    if (!overflow && lane == 0) {
-      sb[cnt] = bT; sa[cnt] = aT;
-      sb[cnt + 1] = bR; sa[cnt + 1] = aR;
-    }
-    const int ncand = cnt + 2;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ---- gift wrap from L to R
-    double bc = bL, ac = aL;
-    for (int guard = 0; guard <= nl && bc < bR; ++guard) {
-      Key3 best = {INFINITY, -INFINITY, -INFINITY};
-      auto consider = [&](double bb, double a) {
-        if (bb > bc) {
-          const double c = (ac - a) / (bb - bc);
-          if (c < best.c || (c == best.c && bb > best.b)) best = {c, bb, a};
-        }
-      };
-      if (!overflow) {
-        for (int e = lane; e < ncand; e += 64) consider(sb[e], sa[e]);
-      } else {
-#pragma unroll
-        for (int t = 0; t < MAXL; ++t)
-          if (lane + 64 * t < nl) consider(lb[t], la[t]);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const double oc = __shfl_xor(best.c, off), ob = __shfl_xor(best.b, off), oa = __shfl_xor(best.a, off);
-        if (oc < best.c || (oc == best.c && ob > best.b)) best = {oc, ob, oa};
-      }
-      if (!(best.b > bc)) break;  // nothing further right (also NaN guard)
-      const double db = best.b - bc;
-      kgj += db * ((best.b <= bT) ? psi(-best.c) : psi(best.c));
-      bc = best.b;
-      ac = best.a;
-      ++hull;
-    }
+    cnt += __popcll(mask);
   }
-  if (nhull != nullptr) *nhull = hull;
-  return kgj;
+  if (cnt + 3 > ENV_CAP) return envelope_walk<MAXL>(la, lb, nl, lane, bL, aL, bR, bT, nhull);
+  if (lane == 0) {
+    sb[cnt] = bL; sa[cnt] = aL;
+    sb[cnt + 1] = bT; sa[cnt + 1] = aT;
+    sb[cnt + 2] = bR; sa[cnt + 2] = aR;
+  }
+  const int nc = cnt + 3;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // ---- every candidate P decides on its own whether it is an envelope line:
+  // P is the max exactly on (cL, cR) with cR = min_{bQ > bP} (aP - aQ)/(bQ - bP)
+  // and cL = max_{bQ < bP} (aQ - aP)/(bP - bQ); it is on the envelope iff
+  // cL < cR and no other candidate has the same slope and a larger intercept
+  // (identical lines: the lowest index keeps it).  Each envelope line other
+  // than R contributes its right edge (P -> argmin Q):
+  //   (bQ - bP) psi(+-cR), minus sign when the edge ends at or left of T.
+  double v = 0.0;
+  int onenv = 0;
+  for (int e = lane; e < nc + 63 - ((nc + 63) % 64) && e < ENV_CAP; e += 64) {
+    const bool mine = e < nc;
+    const double bP = mine ? sb[e] : 0.0, aP = mine ? sa[e] : 0.0;
+    double rn = INFINITY, rd = 1.0, rb = INFINITY;  // right: min (aP - aQ)/(bQ - bP); rb = bQ of the argmin
+    double ln = -INFINITY, ld = 1.0;                // left: max (aQ - aP)/(bP - bQ)
+    bool dominated = false;
+#pragma unroll 4
+    for (int j = 0; j < nc; ++j) {
+      const double bQ = sb[j], aQ = sa[j];
+      // right neighbour candidate: (aP - aQ)/(bQ - bP) over bQ > bP, argmin, ties -> larger bQ
+      const double num = aP - aQ, den = bQ - bP;
+      const double x = num * rd, y = rn * den;
+      const bool right = bQ > bP && (rb == INFINITY || x < y || (x == y && bQ > rb));
+      rn = right ? num : rn;
+      rd = right ? den : rd;
+      rb = right ? bQ : rb;
+      // left: max (aQ - aP)/(bP - bQ) over bQ < bP
+      const double lnum = aQ - aP, lden = bP - bQ;
+      const bool left = bQ < bP && (ln == -INFINITY || lnum * ld > ln * lden);
+      ln = left ? lnum : ln;
+      ld = left ? lden : ld;
+      dominated = dominated || (bQ == bP && (aQ > aP || (aQ == aP && j < e)));
+    }
+    // cL < cR  <=>  ln/ld < rn/rd (both denominators > 0; infinities bracket L and R)
+    const bool env = mine && !dominated && (ln == -INFINITY || rb == INFINITY || ln * rd < rn * ld);
+    if (env && rb != INFINITY) {
+      const double c = rn / rd;
+      v += (rb - bP) * psi((rb <= bT) ? -c : c);
+    }
+    onenv += env ? 1 : 0;
+  }
+  if (nhull) {
+    int hsum = onenv;
+    hsum += __shfl_xor(hsum, 1); hsum += __shfl_xor(hsum, 2); hsum += __shfl_xor(hsum, 4);
+    hsum += __shfl_xor(hsum, 8); hsum += __shfl_xor(hsum, 16); hsum += __shfl_xor(hsum, 32);
+    *nhull = hsum;
+  }
+  return wave_sum(v);
 }
 
-template <int MAXL>
-__global__ __launch_bounds__(512) void envelope_kernel(EnvArgs args) {
-  __shared__ double sv[DKG_MAX_OUTPUTS];   // noiseless posterior variance at x_b per output
-  __shared__ double smx[DKG_MAX_OUTPUTS];  // posterior mean at x_b per output (model space)
-  __shared__ double wsum[16];              // per-wave partial KG sums
-  extern __shared__ __attribute__((aligned(16))) double sbuf[];  // [waves][2][ENV_CAP]
+// Debug phase stamps (debug_flags & 4): [wave][8] s_memtime values.
+constexpr int STAMP_WAVES = 4096;
+__device__ unsigned long long g_stamps[STAMP_WAVES * 8];
+#define DKG_STAMP(k)                                                                              \
+  do {                                                                                            \
+    if ((dbg & 4) && lane == 0) {                                                    \
+      const int sw_ = ((blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wave);         \
+      if (sw_ < STAMP_WAVES) g_stamps[sw_ * 8 + (k)] = __builtin_amdgcn_s_memtime();              \
+    }                                                                                             \
+  } while (0)
 
+// Padded length (doubles) of one LDS-staged line array: whole 1 KiB DMA pieces.
+__host__ __device__ inline int stage_len(int N) { return ((N + 127) / 128) * 128; }
+
+// Async global -> LDS copy of n doubles (16 B per lane per wave instruction,
+// global_load_lds_dwordx4): the data never touches VGPRs and every piece of
+// every wave is in flight at once.  `dst` has stage_len(n) doubles of room.
+__device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, double* dst, int n, int wave, int nwaves,
+                                           int lane) {
+  const int chunks = (n + 1) / 2;  // 16-byte pieces
+  for (int c0 = wave * 64; c0 < chunks; c0 += nwaves * 64) {
+    const int c = min(c0 + lane, chunks - 1);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + 2 * c),
+                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                         reinterpret_cast<uintptr_t>(dst + 2 * c0)),
+                                     16, 0, 0);
+  }
+}
+
+template <int MAXL, int M>
+__global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
+                                                       double* __restrict__ pairs_out) {
+  __shared__ double s_tail[16];
+  __shared__ double s_sv[DKG_MAX_OUTPUTS];   // noiseless posterior variance at x_b, per output
+  __shared__ double s_mx[DKG_MAX_OUTPUTS];   // posterior mean at x_b (model space), per output
+  extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   const int g = blockIdx.y;
   const int SW = blockDim.x >> 6;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int m = args.m;
-  const int N = args.N;
-  const int S = args.S;
-  const int B = args.B;
+  const int m = P->m;  // <= M
+  const int N = P->N;
+  const int NL = N + 1;
+  const int S = P->S;
+  const int target = P->target;
+  const int dbg = P->debug_env;
+  const bool full = target < 0;
+  const int SL = stage_len(N);
+  DKG_STAMP(0);
 
-  // ---- per-candidate posterior variance v_i = s_i - |Q_i[b]|^2 and mean
-  for (int oi = wave; oi < m; oi += SW) {
-    const dkg_output& o = args.outs.o[oi];
-    const int KB = pad16(o.n) / 4;
-    const double* q = args.q[oi] + (size_t)(b >> 4) * KB * 64 + (b & 15);
-    double acc = 0.0;
-    for (int e = lane; e < KB * 4; e += 64) {
-      const double v = q[(size_t)(e >> 2) * 64 + 16 * (e & 3)];
-      acc = fma(v, v, acc);
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      sv[oi] = o.outputscale - acc;
-      smx[oi] = args.mux[oi][b];
+  // Per-output scalars, hoisted once (static kernarg offsets).
+  double ysd[M], ymu[M], nz[M], os[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    ysd[i] = P->o[i].y_std;
+    ymu[i] = P->o[i].y_mean;
+    nz[i] = P->o[i].noise;
+    os[i] = P->o[i].outputscale;
+  }
+
+  // LDS: [pad][mu_i over D] per output, [pad][cov_i over D] per output (line
+  // k >= 1 reads index k - 1; the pad makes the lane-0 / slot-0 read legal),
+  // the weights, then the per-wave survivor lists.
+  const int SLp = SL + 2;
+  double* lmu = smem + 2;
+  double* lcv = lmu + (size_t)M * SLp;
+  double* lw = lcv + (size_t)M * SLp;
+  double* sbuf = lw + ((S * m + 1) & ~1);
+
+  // ---- one round of memory traffic: DMA the line data, plain loads for the rest
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    if (i < m) {
+      dma_to_lds(P->o[i].disc_mean, lmu + (size_t)i * SLp, N, wave, SW, lane);
+      if (full || i == target) dma_to_lds(P->cov[i] + (size_t)b * N, lcv + (size_t)i * SLp, N, wave, SW, lane);
     }
   }
+  for (int e = threadIdx.x; e < S * m; e += blockDim.x) lw[e] = P->weights[e];
+  // candidate's own posterior: v_i = s_i - |Q_i[b]|^2 (wave i), mean from the cross stage
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    if (i < m && wave == i % SW) {
+      const int KB = pad16(P->o[i].n) / 4;
+      const double* q = P->q[i] + (size_t)(b >> 4) * KB * 64 + (b & 15);
+      double acc = 0.0;
+      for (int base = lane; base < KB * 4; base += 8 * 64) {
+        double vq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = min(base + 64 * u, KB * 4 - 1);
+          vq[u] = (base + 64 * u < KB * 4) ? q[(size_t)(e >> 2) * 64 + 16 * (e & 3)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = fma(vq[u], vq[u], acc);
+      }
+      const double mx = P->mux[i][b];
+      acc = wave_sum(acc);
+      if (lane == 0) {
+        s_sv[i] = os[i] - acc;
+        s_mx[i] = mx;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  DKG_STAMP(1);
 
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
   double* sa = sb + ENV_CAP;
   double wave_acc = 0.0;
   const int waves_total = SW * gridDim.y;
+  double sv[M], mx0[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    sv[i] = (i < m) ? s_sv[i] : 0.0;
+    mx0[i] = (i < m) ? s_mx[i] : 0.0;
+  }
 
   for (int j = g * SW + wave; j < S; j += waves_total) {
-    // ---- lines in registers: a = a_off + sum_i wa_i mu_i, b = sum_i wb_i cov_i
-    const bool full = args.target < 0;
+    // ---- line coefficients (wave uniform)
+    double w[M], wa[M], wb[M];
     double a_off = 0.0, den = 0.0;
-    for (int i = 0; i < m; ++i) {
-      const dkg_output& o = args.outs.o[i];
-      const double w = args.weights[(size_t)j * m + i];
-      a_off = fma(w, o.y_mean, a_off);
-      if (full) den = fma(w * w, o.y_std * o.y_std * (sv[i] + o.noise), den);
-    }
-    const double inv_den = full ? 1.0 / sqrt(den) : 0.0;
-    double la[MAXL], lb[MAXL];
 #pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      la[t] = (lane + 64 * t <= N) ? a_off : -INFINITY;
-      lb[t] = 0.0;
+    for (int i = 0; i < M; ++i) {
+      w[i] = (i < m) ? lw[j * m + i] : 0.0;
+      wa[i] = w[i] * ysd[i];
+      a_off = fma(w[i], ymu[i], a_off);
+      den = fma(w[i] * w[i], ysd[i] * ysd[i] * (sv[i] + nz[i]), den);
     }
-#pragma unroll 1
-    for (int i = 0; i < m; ++i) {
-      const dkg_output& o = args.outs.o[i];
-      const double w = args.weights[(size_t)j * m + i];
-      const double sd2 = o.y_std * o.y_std;
-      const double wa = w * o.y_std;
-      double wb = 0.0;
-      if (full) wb = w * w * sd2 * inv_den;
-      else if (i == args.target) wb = w * sd2 / sqrt(sd2 * (sv[i] + o.noise));
-      const double* mu = o.disc_mean - 1;
-      const double* cv = args.cov[i] + (size_t)b * N - 1;
-      const double mu0 = smx[i], cv0 = sv[i];
+    if (full) {
+      const double inv_den = 1.0 / sqrt(den);
 #pragma unroll
-      for (int t = 0; t < MAXL; ++t) {
-        const int k = lane + 64 * t;
-        if (k <= N) {
-          la[t] = fma(wa, (k == 0) ? mu0 : mu[k], la[t]);
-          if (wb != 0.0) lb[t] = fma(wb, (k == 0) ? cv0 : cv[k], lb[t]);
-        }
+      for (int i = 0; i < M; ++i) wb[i] = w[i] * w[i] * ysd[i] * ysd[i] * inv_den;
+    } else {
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const double sd2 = ysd[i] * ysd[i];
+        wb[i] = (i == target) ? w[i] * sd2 / sqrt(sd2 * (sv[i] + nz[i])) : 0.0;
       }
     }
+    // ---- lines: slot t of lane l is line k = l + 64 t (k = 0: the candidate).
+    // Branch-free bodies (one LDS read stream per array, no per-slot waits):
+    // unused output slots read output 0 with a zero weight.
+    const double* mup[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) mup[i] = lmu + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
+    double la[MAXL], lb[MAXL];
+    if (full) {
+      const double* cvp[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) cvp[i] = lcv + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) {
+        double a = a_off, bb = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          a = fma(wa[i], mup[i][64 * t], a);
+          bb = fma(wb[i], cvp[i][64 * t], bb);
+        }
+        la[t] = a;
+        lb[t] = bb;
+      }
+    } else {
+      const double* cvt = lcv + (size_t)target * SLp + lane - 1;
+      double wbt = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) {
+        double a = a_off;
+#pragma unroll
+        for (int i = 0; i < M; ++i) a = fma(wa[i], mup[i][64 * t], a);
+        la[t] = a;
+        lb[t] = wbt * cvt[64 * t];
+      }
+    }
+    {
+      double a = a_off, bb = 0.0;  // line 0: the candidate itself (discretekg.py:182-183)
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        a = fma(wa[i], mx0[i], a);
+        bb = fma(wb[i], sv[i], bb);
+      }
+      la[0] = (lane == 0) ? a : la[0];
+      lb[0] = (lane == 0) ? bb : lb[0];
+    }
+    {  // padding lines beyond N: never maximal, never change min/max slope
+      const double bfill = __shfl(lb[0], 0);
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) {
+        const bool pad = lane + 64 * t > N;
+        la[t] = pad ? -INFINITY : la[t];
+        lb[t] = pad ? bfill : lb[t];
+      }
+    }
+    DKG_STAMP(2);
 
-    const double kgj = envelope_kg<MAXL>(la, lb, N + 1, lane, sb, sa, nullptr);
-    if (args.pairs_out != nullptr && lane == 0) args.pairs_out[(size_t)b * S + j] = kgj;
+    double kgj;
+    if (dbg & 1) {  // ablation: lines + one reduction only
+      double mxv = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) mxv = fmax(mxv, la[t] + lb[t]);
+      kgj = wave_max(mxv);
+    } else {
+      kgj = envelope_kg<MAXL>(la, lb, NL, lane, sb, sa, nullptr);
+    }
+    DKG_STAMP(3);
+    if (pairs_out != nullptr && lane == 0) pairs_out[(size_t)b * S + j] = kgj;
     wave_acc += kgj;
   }
 
-  // ---- deterministic mean over S: per-wave sums -> per-WG sum -> last WG sums the WG partials
-  if (lane == 0) wsum[wave] = wave_acc;
+  // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
+  if (lane == 0) s_tail[wave] = wave_acc;
   __syncthreads();
+  DKG_STAMP(4);
   if (threadIdx.x == 0) {
     double s = 0.0;
-    for (int w = 0; w < SW; ++w) s += wsum[w];
-    if (gridDim.y == 1) {
-      args.kg[b] = s / (double)S;
+    for (int w2 = 0; w2 < SW; ++w2) s += s_tail[w2];
+    const int G = gridDim.y;
+    if (G == 1) {
+      kg[b] = s / (double)S;
+    } else if (G == 2 || (dbg & 2)) {
+      // two addends onto a zeroed cell: fp addition commutes, so the order
+      // the two workgroups arrive in does not change the bits.
+      atomicAdd(&kg[b], s / (double)S);
     } else {
-      args.wg_part[(size_t)b * gridDim.y + g] = s;
+      P->wg_part[(size_t)b * G + g] = s;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int prev = atomicAdd(&args.tickets[b], 1);
-      if (prev == (int)gridDim.y - 1) {
+      const int prev = atomicAdd(&P->tickets[b], 1);
+      if (prev == G - 1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         double tot = 0.0;
-        for (int q = 0; q < (int)gridDim.y; ++q)
-          tot += __hip_atomic_load(&args.wg_part[(size_t)b * gridDim.y + q], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        args.kg[b] = tot / (double)S;
+        for (int q = 0; q < G; ++q)
+          tot += __hip_atomic_load(&P->wg_part[(size_t)b * G + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        kg[b] = tot / (double)S;
       }
     }
   }
-  (void)B;
+  __syncthreads();
+  DKG_STAMP(5);
+}
+
+static int outputs_bucket(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 3 ? 3 : m <= 4 ? 4 : 8; }
+
+size_t envelope_lds_bytes(int m, int N, int waves, int S) {
+  const int M = outputs_bucket(m);
+  return ((size_t)2 + 2 * (size_t)M * (stage_len(N) + 2) + ((S * m + 1) & ~1) + (size_t)waves * 2 * ENV_CAP) *
+         sizeof(double);
 }
 
 // ---------------------------------------------------------------------------
@@ -441,9 +708,9 @@ __global__ __launch_bounds__(256) void lines_kg_kernel(const double* __restrict_
   double la[MAXL], lb[MAXL];
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
-    const int k = lane + 64 * t;
-    la[t] = (k < L) ? a[(size_t)p * L + k] : -INFINITY;
-    lb[t] = (k < L) ? b[(size_t)p * L + k] : 0.0;
+    const int k = min(lane + 64 * t, L - 1);
+    la[t] = a[(size_t)p * L + k];
+    lb[t] = b[(size_t)p * L + k];
   }
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
   int h = 0;
@@ -463,6 +730,21 @@ __global__ void debug_mfma_kernel(const double* __restrict__ a, const double* __
   for (int r = 0; r < 4; ++r) c[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
 }
 
+// Self-test of the register butterflies: out[64 s + l] = partner_f64<s>(in[l])
+// for s = 0..5, out[384 + l] = wave_sum(in), out[448 + l] = wave_max(in).
+__global__ void debug_wave_kernel(const double* __restrict__ in, double* __restrict__ out) {
+  const int l = threadIdx.x;
+  const double v = in[l];
+  out[0 * 64 + l] = partner_f64<0>(v);
+  out[1 * 64 + l] = partner_f64<1>(v);
+  out[2 * 64 + l] = partner_f64<2>(v);
+  out[3 * 64 + l] = partner_f64<3>(v);
+  out[4 * 64 + l] = partner_f64<4>(v);
+  out[5 * 64 + l] = partner_f64<5>(v);
+  out[6 * 64 + l] = wave_sum(v);
+  out[7 * 64 + l] = wave_max(v);
+}
+
 // ---------------------------------------------------------------------------
 // Launch helpers (host).
 hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, int n1, const double* x2, int n2,
@@ -479,40 +761,84 @@ hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_cross_root(const CrossArgs& a, int m, int max_np, hipStream_t s) {
-  const int T = max_np / 16;
-  dim3 grid(pad16(a.rows) / 16, (T + 1) / 2, m);
-  hipLaunchKernelGGL(cross_root_kernel, grid, dim3(CR_WAVES * WAVE), cross_root_lds_bytes(max_np), s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_posterior_cov(const CovArgs& a, int m, hipStream_t s) {
-  dim3 grid(pad16(a.N) / 16, pad16(a.B) / 16, m);
-  hipLaunchKernelGGL(posterior_cov_kernel, grid, dim3(PC_WAVES * WAVE), 0, s, a);
+hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s) {
+  const int np = pad16(a.o.n);
+  dim3 grid(pad16(a.rows) / 16, (np / 16 + 1) / 2, 1);
+  const size_t lds = cross_root_lds_bytes(np, a.d);
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)cross_root_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(cross_root_kernel, grid, dim3(CR_WAVES * WAVE), lds, s, a);
   return hipGetLastError();
 }
 
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {
-  // Aim for >= 512 workgroups (2 per CU) while keeping up to 8 scalarisation
-  // waves of one candidate together.
-  int sw = std::max(1, std::min(8, S));
-  while (sw > 1 && (long)B * ((S + sw - 1) / sw) < 512) sw /= 2;
+  // Up to 8 scalarisation waves of one candidate per workgroup; with S <= 16
+  // at most two workgroups per candidate, whose partial sums meet in one
+  // commutative atomic add (no inter-workgroup fences).
+  (void)B;
+  const int sw = std::max(1, std::min(8, S));
   *waves_per_wg = sw;
   *split = (S + sw - 1) / sw;
 }
 
-hipError_t launch_envelope(const EnvArgs& a, int sw, int split, hipStream_t s) {
-  dim3 grid(a.B, split);
-  dim3 block(sw * WAVE);
-  const size_t lds = (size_t)sw * 2 * ENV_CAP * sizeof(double);
-  const int lines = a.N + 1;
-  if (lines <= 64 * 2) hipLaunchKernelGGL(envelope_kernel<2>, grid, block, lds, s, a);
-  else if (lines <= 64 * 4) hipLaunchKernelGGL(envelope_kernel<4>, grid, block, lds, s, a);
-  else if (lines <= 64 * 8) hipLaunchKernelGGL(envelope_kernel<8>, grid, block, lds, s, a);
-  else if (lines <= 64 * 17) hipLaunchKernelGGL(envelope_kernel<17>, grid, block, lds, s, a);
-  else if (lines <= 64 * 33) hipLaunchKernelGGL(envelope_kernel<33>, grid, block, lds, s, a);
-  else return hipErrorInvalidValue;
+template <int MAXL, int M>
+static hipError_t launch_env_t(const Plan* dev, int B, double* kg, double* pairs, dim3 grid, dim3 block, size_t lds,
+                               hipStream_t s) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL((envelope_kernel<MAXL, M>), grid, block, lds, s, dev, B, kg, pairs);
   return hipGetLastError();
+}
+
+template <int M>
+static hipError_t launch_env_m(int lines, const Plan* dev, int B, double* kg, double* pairs, dim3 grid, dim3 block,
+                               size_t lds, hipStream_t s) {
+  if (lines <= 64 * 2) return launch_env_t<2, M>(dev, B, kg, pairs, grid, block, lds, s);
+  if (lines <= 64 * 4) return launch_env_t<4, M>(dev, B, kg, pairs, grid, block, lds, s);
+  if (lines <= 64 * 8) return launch_env_t<8, M>(dev, B, kg, pairs, grid, block, lds, s);
+  if (lines <= 64 * 17) return launch_env_t<17, M>(dev, B, kg, pairs, grid, block, lds, s);
+  if (lines <= 64 * 33) return launch_env_t<33, M>(dev, B, kg, pairs, grid, block, lds, s);
+  return hipErrorInvalidValue;
+}
+
+// The three launches of one forward on `s`; ev (nullable) gets 4 events
+// recorded around them (dkg_forward_timed).
+hipError_t launch_forward(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
+                          hipStream_t s, hipEvent_t* ev) {
+  if (ev) (void)hipEventRecord(ev[0], s);
+  {
+    dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m);
+    const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+    hipLaunchKernelGGL(cross_root_plan_kernel, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (ev) (void)hipEventRecord(ev[1], s);
+  if (h.N > 0) {
+    dim3 grid(pad16(h.N) / 16, pad16(B) / 16, h.m);
+    hipLaunchKernelGGL(posterior_cov_kernel, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (ev) (void)hipEventRecord(ev[2], s);
+  {
+    dim3 grid(B, h.split), block(h.sw * WAVE);
+    const size_t lds = envelope_lds_bytes(h.m, h.N, h.sw, h.S);
+    hipError_t e;
+    switch (outputs_bucket(h.m)) {
+      case 1: e = launch_env_m<1>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
+      case 2: e = launch_env_m<2>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
+      case 3: e = launch_env_m<3>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
+      case 4: e = launch_env_m<4>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
+      default: e = launch_env_m<8>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
+    }
+    if (e != hipSuccess) return e;
+  }
+  if (ev) (void)hipEventRecord(ev[3], s);
+  return hipSuccess;
 }
 
 hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s) {
@@ -525,6 +851,15 @@ hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, doubl
   else if (L <= 64 * 17) hipLaunchKernelGGL(lines_kg_kernel<17>, grid, block, lds, s, a, b, P, L, kg, nhull);
   else if (L <= 64 * 33) hipLaunchKernelGGL(lines_kg_kernel<33>, grid, block, lds, s, a, b, P, L, kg, nhull);
   else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t read_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * std::min(n, STAMP_WAVES * 8));
+}
+
+hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(debug_wave_kernel, dim3(1), dim3(64), 0, s, in, out);
   return hipGetLastError();
 }
 

@@ -57,7 +57,16 @@ SIGNATURES = {
     "dkg_forward_timed": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                                   POINTER(c_float)]),
+    "dkg_plan_bytes": (c_size_t, []),
+    "dkg_plan_workspace": (c_size_t, [POINTER(DkgOutput), c_int, c_int, c_int, c_int]),
+    "dkg_plan_init": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                              c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+    "dkg_plan_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_plan_forward_timed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                       POINTER(c_float)]),
     "dkg_lines_kg": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_debug_read_stamps": (c_int, [c_void_p, c_int]),
+    "dkg_debug_wave_ops": (c_int, [c_void_p, c_void_p, c_void_p]),
     "dkg_debug_mfma_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 

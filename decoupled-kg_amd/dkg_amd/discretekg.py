@@ -74,8 +74,8 @@ class _ForwardFn(torch.autograd.Function):
     """Device forward; the closed-form backward is not wired in yet."""
 
     @staticmethod
-    def forward(ctx, X, state, W, target):
-        return state.forward(X, W, target)
+    def forward(ctx, X, acq):
+        return acq._plan_for(X.shape[0]).forward(X)
 
     @staticmethod
     def backward(ctx, grad):  # pragma: no cover
@@ -131,6 +131,16 @@ class DiscreteKnowledgeGradient(_Base):
         self.target_output_ix = target_output_ix
         self._state = DeviceGPState(state, x_discretisation, device)
         self._W = scalarisation_weights.detach().to(self._state.device, torch.double).contiguous()
+        self._plan = None
+
+    def _plan_for(self, B: int):
+        """The forward plan, grown (powers of two) to hold B candidates."""
+        if self._plan is None or self._plan.max_B < B:
+            cap = 1
+            while cap < B:
+                cap *= 2
+            self._plan = self._state.plan(self._W, self.target_output_ix, max(cap, 16))
+        return self._plan
 
     def set_X_pending(self, X_pending: Optional[Tensor] = None) -> None:
         raise UnsupportedError(f"{type(self).__name__} does not account for X_pending yet.")
@@ -143,14 +153,14 @@ class DiscreteKnowledgeGradient(_Base):
                 f"Expected X to have last dimension matching 'self.x_discretisation'. "
                 f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
         flat = X.reshape(-1, d)
-        kg = _ForwardFn.apply(flat, self._state, self._W, self.target_output_ix)
+        kg = _ForwardFn.apply(flat, self)
         return kg.to(device=X.device, dtype=X.dtype).reshape(batch_shape)
 
     def forward_pairs(self, X: Tensor) -> Tensor:
         """KG per (candidate, scalarisation): [B, S] (the per-``j`` values of ``:200-233``)."""
         flat = X.reshape(-1, X.shape[-1])
         pairs = torch.empty(flat.shape[0], self._W.shape[0], dtype=torch.double, device=self._state.device)
-        self._state.forward(flat, self._W, self.target_output_ix, kg_pairs=pairs)
+        self._plan_for(flat.shape[0]).forward(flat, kg_pairs=pairs)
         return pairs
 
 

@@ -19,6 +19,7 @@ same caches once per BO iteration — and stays in HBM for every forward call.
 
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 from typing import List
 
@@ -143,29 +144,61 @@ class DeviceGPState:
         self._ws = None
         self._ws_key = None
 
-    def workspace(self, B: int, S: int) -> torch.Tensor:
-        lib = _lib.load()
-        need = lib.dkg_forward_workspace(self.structs, self.m, self.N, B, S)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
-        return self._ws
+    def plan(self, W: torch.Tensor, target, max_B: int) -> "ForwardPlan":
+        return ForwardPlan(self, W, target, max_B)
 
     def forward(self, X: torch.Tensor, W: torch.Tensor, target, kg_pairs=None, timed: bool = False):
-        """kg[B] for candidates X (device, B x d) and weights W (device, S x m)."""
+        """One-shot forward (builds a plan on the fly); see ForwardPlan for the fast path."""
+        p = ForwardPlan(self, W, target, max(1, X.shape[0]))
+        return p.forward(X, kg_pairs=kg_pairs, timed=timed)
+
+
+class ForwardPlan:
+    """A DKG plan (include/dkg.h "Plan API"): weights, target and workspace for
+    up to ``max_B`` candidates, device copy written once; ``forward`` is one
+    C call that launches the three kernels on the current stream."""
+
+    def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int):
         lib = _lib.load()
+        self.state = state
+        self.device = state.device
+        self.W = W.detach().to(self.device, torch.double).contiguous()
+        if self.W.dim() != 2 or self.W.shape[1] != state.m:
+            raise ValueError(f"weights must be S x {state.m}")
+        self.S = self.W.shape[0]
+        self.target = -1 if target is None else int(target)
+        self.max_B = int(max_B)
+        need = lib.dkg_plan_workspace(state.structs, state.m, state.N, self.max_B, self.S)
+        self.ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
+        nbytes = lib.dkg_plan_bytes()
+        self.host = ctypes.create_string_buffer(nbytes)
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        _lib.check(lib.dkg_plan_init(state.structs, state.m, state.d, _lib.ptr(state.D), state.N, _lib.ptr(self.W),
+                                     self.S, self.target, self.max_B, _lib.ptr(self.ws), self.ws.numel(),
+                                     self.host, _lib.ptr(self.dev), current_stream_ptr(self.device)),
+                   "dkg_plan_init")
+        self._fwd = lib.dkg_plan_forward
+        self._fwd_timed = lib.dkg_plan_forward_timed
+        self._dev_ptr = _lib.ptr(self.dev)
+
+    def forward_into(self, X: torch.Tensor, kg: torch.Tensor, kg_pairs=None) -> None:
+        """Hot path: X (device, B x d, contiguous fp64) -> kg (device, B)."""
+        st = self._fwd(self.host, self._dev_ptr, X.data_ptr(), X.shape[0], kg.data_ptr(),
+                       0 if kg_pairs is None else kg_pairs.data_ptr(),
+                       torch.cuda.current_stream(self.device).cuda_stream)
+        if st:
+            _lib.check(st, "dkg_plan_forward")
+
+    def forward(self, X: torch.Tensor, kg_pairs=None, timed: bool = False):
         X = X.detach().to(self.device, torch.double).contiguous()
-        W = W.detach().to(self.device, torch.double).contiguous()
         B = X.shape[0]
-        S = W.shape[0]
+        if B > self.max_B:
+            raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
         kg = torch.empty(B, dtype=torch.double, device=self.device)
-        ws = self.workspace(B, S)
-        stream = current_stream_ptr(self.device)
-        tgt = -1 if target is None else int(target)
-        args = (self.structs, self.m, self.d, _lib.ptr(self.D), self.N, _lib.ptr(X), B, _lib.ptr(W), S, tgt,
-                _lib.ptr(kg), _lib.ptr(kg_pairs), _lib.ptr(ws), ws.numel(), stream)
         if timed:
             ms = (_lib.c_float * 3)()
-            _lib.check(lib.dkg_forward_timed(*args, ms), "dkg_forward_timed")
+            _lib.check(self._fwd_timed(self.host, self._dev_ptr, _lib.ptr(X), B, _lib.ptr(kg), _lib.ptr(kg_pairs),
+                                       current_stream_ptr(self.device), ms), "dkg_plan_forward_timed")
             return kg, list(ms)
-        _lib.check(lib.dkg_forward(*args), "dkg_forward")
+        self.forward_into(X, kg, kg_pairs)
         return kg

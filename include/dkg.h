@@ -120,6 +120,28 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
                       int B, const double* weights, int S, int target, double* kg, double* kg_pairs,
                       void* workspace, size_t workspace_bytes, void* stream, float* stage_ms);
 
+/* ---- Plan API (the fast path) -------------------------------------------
+ * A plan is everything a forward needs besides the candidates: the m output
+ * states, the discretisation, the weights, the target and the workspace carve
+ * for up to max_B candidates.  dkg_plan_init validates it, writes it to
+ * `host_plan` (caller memory of dkg_plan_bytes() bytes, kept unchanged while
+ * the plan is in use) and copies it to `dev_plan` (device memory of the same
+ * size) on `stream`.  dkg_plan_forward then launches the three kernels with a
+ * pointer to the device copy (no per-call host-to-device traffic).  The
+ * disc/weights/workspace buffers must outlive the plan. */
+size_t dkg_plan_bytes(void);
+size_t dkg_plan_workspace(const dkg_output* outs, int m, int N, int max_B, int S);
+int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
+                  int target, int max_B, void* workspace, size_t workspace_bytes, void* host_plan, void* dev_plan,
+                  void* stream);
+/* kg[b] (and kg_pairs[b x S], nullable) for B <= max_B candidates xnew (device, B x d);
+ * same result as dkg_forward with the plan's arguments. */
+int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                     double* kg_pairs, void* stream);
+/* As dkg_plan_forward with per-kernel HIP-event timings (synchronises): stage_ms[3]. */
+int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                           double* kg_pairs, void* stream, float* stage_ms);
+
 /* Envelope stage alone: for P independent sets of L lines a_k + b_k z
  * (device, row-major [P][L]) kg[p] = E[max_k (a_k + b_k Z)] - max_k a_k, Z ~ N(0,1),
  * and optionally the number of upper-envelope lines n_hull[p] (nullable).
@@ -128,6 +150,16 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
  * L = 0 -> DKG_ERR_NO_LINES (the reference's ValueError, :466-470). */
 int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,
                  void* stream);
+
+/* Debug: copy the envelope kernel's phase stamps (written when the env var
+ * DKG_DEBUG_ENV_FLAGS has bit 4 set at plan creation) to host memory: n words. */
+int dkg_debug_read_stamps(unsigned long long* host, int n);
+
+/* Debug/self-test of the register-only wave butterflies the kernels use
+ * (DPP + v_permlane16/32_swap): in[64] -> out[512]; out[64 s + l] is the
+ * partner value lane l receives at butterfly step s (0..5), out[384 + l] the
+ * wave sum and out[448 + l] the wave max seen by lane l. */
+int dkg_debug_wave_ops(const double* in, double* out, void* stream);
 
 /* Debug/self-test: C[16x16] = A[16x4] B[4x16] (row-major, device) with one
  * v_mfma_f64_16x16x4_f64 using the operand/result lane maps the kernels assume. */

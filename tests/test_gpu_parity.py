@@ -297,3 +297,23 @@ def test_lines_match_oracle_lines_headline():
                        for i in range(a.shape[0])])
     assert_kg_close(got, ref, 64 * torch.finfo(torch.double).eps * a.abs().amax(-1))
     del DiscreteKnowledgeGradient
+
+
+def test_wave_butterfly_primitives():
+    """DPP + permlane butterfly steps pair every lane with the mirror lane of the other half-group."""
+    from dkg_amd import _lib
+
+    lib = _lib.load()
+    x = torch.arange(64, dtype=torch.double) * 3.0 + 1.0
+    xin = x.to(DEV)
+    out = torch.empty(512, dtype=torch.double, device=DEV)
+    _lib.check(lib.dkg_debug_wave_ops(_lib.ptr(xin), _lib.ptr(out), 0), "debug_wave")
+    torch.cuda.synchronize()
+    o = out.cpu().reshape(8, 64)
+    lanes = torch.arange(64)
+    expected_partner = [lanes ^ 1, lanes ^ 2, (lanes & ~7) | (7 - (lanes & 7)), (lanes & ~15) | (15 - (lanes & 15)),
+                        lanes ^ 16, lanes ^ 32]
+    for s, p in enumerate(expected_partner):
+        assert torch.equal(o[s], x[p]), f"step {s}: got lanes {((o[s] - 1) / 3).long().tolist()}"
+    assert torch.equal(o[6], torch.full((64,), float(x.sum()), dtype=torch.double))
+    assert torch.equal(o[7], torch.full((64,), float(x.max()), dtype=torch.double))
