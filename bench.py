@@ -7,7 +7,11 @@ S=16 scalarisations, B=128 candidates per GPU, d=2, fp64.  Inputs and GP state
 are resident in HBM before timing.  For N>1 (torchrun, one rank per GPU,
 RCCL) each rank evaluates its own 128 candidates (weak scaling) and the
 per-candidate KG values are all-gathered every step (async, double
-buffered), so every rank ends with the whole batch.
+buffered), so every rank ends with the whole batch.  ``--shard scalarisations``
+instead gives every rank the same 128 candidates and its own 16 weight rows
+(16*N in total) and combines per-candidate partial sums with one async RCCL
+all-reduce per step (the north-star exchange); ``value`` then
+counts headline-equivalent evals (candidates x 16 scalarisations).
 
 Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus the
 roofline of the dominant kernel (HIP-event timed, same stream) and a bounded
@@ -39,6 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="headline")
+    ap.add_argument("--shard", choices=["candidates", "scalarisations"], default="candidates",
+                    help="axis of the (candidate x scalarisation) space split over ranks (weak scaling)")
     ap.add_argument("--target", type=int, default=None, help="target_output_ix (decoupled path); default full")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -79,12 +85,12 @@ def cpu_baseline(model, D, W, X, target, seconds, threads):
     one(Xc[0])  # warm-up (builds the per-model caches, as GPyTorch does on first call)
     t0 = time.perf_counter()
     cnt = 0
-    while cnt < Xc.shape[0] and (time.perf_counter() - t0 < seconds or cnt < 4):
-        one(Xc[cnt])
+    while time.perf_counter() - t0 < seconds or cnt < 4:
+        one(Xc[cnt % Xc.shape[0]])
         cnt += 1
     dt = time.perf_counter() - t0
     return {"value": cnt / dt, "unit": "KG-evals/s", "cores": threads, "kind": "port",
-            "sample": f"{cnt} of the {Xc.shape[0]} headline candidates, one forward each (per-candidate loop, "
+            "sample": f"{cnt} forwards cycling over the {Xc.shape[0]} headline candidates (per-candidate loop, "
                       f"dense (N+1)^2 posterior covariance, reference epigraph walk; torch fp64 CPU), "
                       f"{dt:.1f} s"}
 
@@ -103,14 +109,21 @@ def main():
 
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
+    from dkg_amd.utils import sample_simplex
 
     w = WORKLOADS[args.workload]
     model, D, X0, W = make_problem(w)
-    # weak scaling: every rank evaluates its own B candidates (Sobol stream per rank)
-    X = torch.quasirandom.SobolEngine(w.d, scramble=True, seed=4 + 1000 * rank).draw(w.B, dtype=torch.double)
-    if rank == 0:
-        X = X0
-    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=args.target, device=dev)
+    X = X0
+    if args.shard == "candidates":
+        # weak scaling: every rank evaluates its own B candidates (Sobol stream per rank)
+        if rank > 0:
+            X = torch.quasirandom.SobolEngine(w.d, scramble=True, seed=4 + 1000 * rank).draw(w.B, dtype=torch.double)
+        W_local = W
+    else:
+        # weak scaling: S rows per rank out of S*world (rank 0's rows are the headline W)
+        W_all = W if world == 1 else torch.cat([W, sample_simplex(w.m, w.S * (world - 1), qmc=True, seed=99)])
+        W_local = W_all[rank * w.S:(rank + 1) * w.S]
+    acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev)
     plan = acq._plan_for(w.B)
     Xd = X.to(dev).contiguous()
     kgs = [torch.empty(w.B, dtype=torch.double, device=dev) for _ in range(2)]
@@ -118,13 +131,17 @@ def main():
     works = [None, None]
 
     def step(k):
-        kg = kgs[k % 2]
+        slot = k % 2
+        kg = kgs[slot]
+        if world > 1 and works[slot] is not None:
+            works[slot].wait()      # the exchange that last used this buffer is done
         plan.forward_into(Xd, kg)
         if world > 1:
-            slot = k % 2
-            if works[slot] is not None:
-                works[slot].wait()
-            works[slot] = dist.all_gather_into_tensor(gathered[slot], kg, async_op=True)
+            if args.shard == "candidates":
+                works[slot] = dist.all_gather_into_tensor(gathered[slot], kg, async_op=True)
+            else:
+                kg.mul_(w.S)        # partial sum over this rank's rows; / (S*world) after the reduce
+                works[slot] = dist.all_reduce(kg, op=dist.ReduceOp.SUM, async_op=True)
         return kg
 
     for k in range(args.warmup):
@@ -155,18 +172,13 @@ def main():
 
     # ---- per-kernel durations (HIP events on the launch stream), roofline of the dominant kernel
     names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
-    acc = [0.0, 0.0, 0.0]
-    for _ in range(args.profile_reps):
-        _, ms = plan.forward(Xd, timed=True)
-        acc = [a + b for a, b in zip(acc, ms)]
-    avg_ms = [a / args.profile_reps for a in acc]
+    avg_ms = [plan.time_stage(Xd, k, args.profile_reps) for k in range(3)]
     model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)
     dom = max(range(3), key=lambda i: avg_ms[i])
     fl, by = model_fb[names[dom]]
-    if names[dom] == "posterior_cov_kernel":
-        bound, ach, peak, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
-    else:
-        bound, ach, peak, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
+    # every stage is fp64-compute bound (DESIGN.md "Roofline"): MFMA for cross/cov, fp64 VALU (same 78.6 TF
+    # peak) for the envelope; HBM bytes per launch are << peak*duration for all three.
+    bound, ach, peak, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
     traffic = None
     if os.path.exists(args.pmc):
         try:
@@ -199,7 +211,9 @@ def main():
             "config": {"workload": args.workload, "m": w.m, "n_train": w.n_train, "n_disc": D.shape[0],
                        "S": w.S, "B_per_gpu": w.B, "d": w.d,
                        "path": "full" if args.target is None else f"target_output_ix={args.target}",
-                       "parallelism": f"candidates sharded over {world} GPU(s); per-step async all-gather"},
+                       "shard": args.shard,
+                       "parallelism": f"{args.shard} sharded over {world} GPU(s); per-step async "
+                                      f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'}"},
             "forward_calls_per_s": world * args.steps / elapsed,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -230,6 +230,34 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
 
 size_t dkg_plan_bytes(void) { return sizeof(Plan); }
 
+int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                        double* kg_pairs, void* stream, int stage, int reps, float* avg_ms) {
+  if (!host_plan || !dev_plan || !avg_ms) return fail(DKG_ERR_ARG, "NULL pointer");
+  if (stage < 0 || stage > 2 || reps < 1) return fail(DKG_ERR_ARG, "stage=%d reps=%d", stage, reps);
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  if (B < 1 || B > h.max_B) return fail(DKG_ERR_ARG, "B=%d outside [1, %d]", B, h.max_B);
+  if (!xnew || !kg) return fail(DKG_ERR_ARG, "NULL data pointer");
+  const Plan* dev = static_cast<const Plan*>(dev_plan);
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t ev[2];
+  int st;
+  for (int k = 0; k < 2; ++k)
+    if ((st = hip_check(hipEventCreate(&ev[k]), "hipEventCreate"))) return st;
+  // prime the inputs of the timed stage, then time reps back-to-back launches of it alone
+  if ((st = hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr), "forward"))) return st;
+  (void)hipEventRecord(ev[0], s);
+  for (int r = 0; r < reps; ++r)
+    if ((st = hip_check(launch_stage(h, dev, xnew, B, kg, kg_pairs, s, stage), "stage"))) return st;
+  (void)hipEventRecord(ev[1], s);
+  if ((st = hip_check(hipEventSynchronize(ev[1]), "hipEventSynchronize"))) return st;
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+  *avg_ms = ms / reps;
+  for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev[k]);
+  // leave kg / kg_pairs valid again (repeated stages accumulate into kg)
+  return hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr), "forward");
+}
+
 size_t dkg_plan_workspace(const dkg_output* outs, int m, int N, int max_B, int S) {
   if (!outs || m < 1 || m > DKG_MAX_OUTPUTS) return 0;
   return layout(outs, m, N, max_B, S).total;

@@ -38,6 +38,9 @@ hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, in
                                 double diag_add, double* out, hipStream_t s);
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
+// One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.
+hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
+                        hipStream_t s, int stage);
 hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                           hipStream_t s, hipEvent_t* ev);
 hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s);

@@ -803,38 +803,39 @@ static hipError_t launch_env_m(int lines, const Plan* dev, int B, double* kg, do
 
 // The three launches of one forward on `s`; ev (nullable) gets 4 events
 // recorded around them (dkg_forward_timed).
-hipError_t launch_forward(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
-                          hipStream_t s, hipEvent_t* ev) {
-  if (ev) (void)hipEventRecord(ev[0], s);
-  {
+hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
+                        hipStream_t s, int stage) {
+  if (stage == 0) {
     dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
     if (lds > 65536)
       (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds);
     hipLaunchKernelGGL(cross_root_plan_kernel, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
   }
-  if (ev) (void)hipEventRecord(ev[1], s);
-  if (h.N > 0) {
+  if (stage == 1) {
+    if (h.N == 0) return hipSuccess;
     dim3 grid(pad16(h.N) / 16, pad16(B) / 16, h.m);
     hipLaunchKernelGGL(posterior_cov_kernel, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
   }
-  if (ev) (void)hipEventRecord(ev[2], s);
-  {
-    dim3 grid(B, h.split), block(h.sw * WAVE);
-    const size_t lds = envelope_lds_bytes(h.m, h.N, h.sw, h.S);
-    hipError_t e;
-    switch (outputs_bucket(h.m)) {
-      case 1: e = launch_env_m<1>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
-      case 2: e = launch_env_m<2>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
-      case 3: e = launch_env_m<3>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
-      case 4: e = launch_env_m<4>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
-      default: e = launch_env_m<8>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s); break;
-    }
+  dim3 grid(B, h.split), block(h.sw * WAVE);
+  const size_t lds = envelope_lds_bytes(h.m, h.N, h.sw, h.S);
+  switch (outputs_bucket(h.m)) {
+    case 1: return launch_env_m<1>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
+    case 2: return launch_env_m<2>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
+    case 3: return launch_env_m<3>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
+    case 4: return launch_env_m<4>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
+    default: return launch_env_m<8>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
+  }
+}
+
+hipError_t launch_forward(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
+                          hipStream_t s, hipEvent_t* ev) {
+  for (int stage = 0; stage < 3; ++stage) {
+    if (ev) (void)hipEventRecord(ev[stage], s);
+    const hipError_t e = launch_stage(h, dev, xnew, B, kg, pairs, s, stage);
     if (e != hipSuccess) return e;
   }
   if (ev) (void)hipEventRecord(ev[3], s);

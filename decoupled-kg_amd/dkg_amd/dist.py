@@ -1,0 +1,117 @@
+"""Multi-GPU Discrete KG: the (candidate x scalarisation) pair space split over ranks.
+
+SURVEY.md §8(e): every (xnew, w) pair is independent (``discretekg.py:200-235``
+loops over scalarisations and averages; ``:145`` loops over candidates), so the
+only exchange is combining per-candidate results:
+
+* ``axis="scalarisations"`` — rank r evaluates all B candidates on its
+  contiguous slice of the S weight rows; the per-candidate partial sums
+  ``S_r * mean_r`` meet in ONE all-reduce (sum, fp64, count B) and are divided
+  by S.  This is the north-star layout (one RCCL all-reduce of per-candidate
+  KG values over xGMI).
+* ``axis="candidates"`` — rank r evaluates its contiguous slice of the B
+  candidates on all S rows; the slices meet in one all-gather.
+
+One process per GPU (``torch.distributed``; backend "nccl" is RCCL on ROCm,
+"gloo" for the CPU tests).  GP state is replicated: each rank builds its
+device caches from the same host tensors.  The local evaluation is
+``DiscreteKnowledgeGradient`` on the rank's device unless ``local_forward``
+is injected (the multi-process CPU tests inject the oracle).
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+from torch import Tensor
+
+from .errors import BotorchTensorDimensionError
+
+LocalForward = Callable[[Tensor, Tensor], Tensor]  # (X [B, d], W [S_r, m]) -> KG averaged over W, [B]
+
+
+def shard_range(total: int, rank: int, world: int) -> tuple:
+    """Contiguous slice [lo, hi) of ``total`` items owned by ``rank`` (chunks of ceil(total/world))."""
+    chunk = -(-total // world) if total > 0 else 0
+    lo = min(total, rank * chunk)
+    return lo, min(total, lo + chunk)
+
+
+class ShardedDiscreteKG:
+    """``DiscreteKnowledgeGradient.forward`` with the pair space split across ranks.
+
+    Every rank calls ``forward`` with the same X and receives the full [*batch]
+    result (the unsharded KG up to fp64 summation order of the S average).
+    """
+
+    AXES = ("scalarisations", "candidates")
+
+    def __init__(self, model, x_discretisation: Tensor, scalarisation_weights: Tensor,
+                 target_output_ix: Optional[int] = None, axis: str = "scalarisations", group=None,
+                 local_forward: Optional[LocalForward] = None, device=None):
+        if axis not in self.AXES:
+            raise ValueError(f"axis must be one of {self.AXES}; got {axis!r}")
+        if scalarisation_weights.dim() != 2:
+            raise BotorchTensorDimensionError("Expected 'scalarisation_weights' to have two dimensions.")
+        self.axis = axis
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.W = scalarisation_weights
+        self.S = scalarisation_weights.shape[0]
+        self.d = x_discretisation.shape[-1]
+        self.w_lo, self.w_hi = shard_range(self.S, self.rank, self.world) if axis == "scalarisations" \
+            else (0, self.S)
+        self.device = torch.device(device) if device is not None else None
+        if local_forward is None:
+            from .discretekg import DiscreteKnowledgeGradient
+            W_local = scalarisation_weights[self.w_lo:self.w_hi]
+            self._acq = None
+            if self.w_hi > self.w_lo:
+                self._acq = DiscreteKnowledgeGradient(model, x_discretisation, W_local, target_output_ix,
+                                                      device=device)
+
+            def local_forward(X, W):  # noqa: ARG001 - W is baked into the plan
+                return self._acq(X.unsqueeze(-2))
+
+        self._local = local_forward
+
+    def _comm_device(self, like: Tensor) -> torch.device:
+        backend = dist.get_backend(self.group) if dist.is_initialized() else "gloo"
+        if backend == "nccl":
+            return self.device or torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def forward(self, X: Tensor) -> Tensor:
+        if X.dim() < 2 or X.shape[-2] != 1:
+            raise AssertionError(f"Expected X to be `batch_shape x q=1 x d`, but got X with shape {X.shape}.")
+        batch_shape = X.shape[:-2]
+        flat = X.reshape(-1, self.d)
+        B = flat.shape[0]
+        cdev = self._comm_device(flat)
+        if self.axis == "scalarisations":
+            part = torch.zeros(B, dtype=torch.double, device=cdev)
+            n_local = self.w_hi - self.w_lo
+            if n_local > 0 and B > 0:
+                part += self._local(flat, self.W[self.w_lo:self.w_hi]).to(cdev, torch.double) * n_local
+            if self.world > 1:
+                dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+            out = part / self.S
+        else:
+            chunk = -(-B // self.world) if B > 0 else 0
+            lo, hi = shard_range(B, self.rank, self.world)
+            mine = torch.zeros(chunk, dtype=torch.double, device=cdev)
+            if hi > lo:
+                mine[: hi - lo] = self._local(flat[lo:hi], self.W).to(cdev, torch.double)
+            if self.world > 1:
+                allv = torch.empty(chunk * self.world, dtype=torch.double, device=cdev)
+                dist.all_gather_into_tensor(allv, mine, group=self.group) if cdev.type == "cuda" else \
+                    dist.all_gather(list(allv.view(self.world, chunk)), mine, group=self.group)
+            else:
+                allv = mine
+            out = allv[:B]
+        return out.to(X.device).reshape(batch_shape)
+
+    __call__ = forward

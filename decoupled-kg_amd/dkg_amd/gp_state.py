@@ -189,6 +189,17 @@ class ForwardPlan:
         if st:
             _lib.check(st, "dkg_plan_forward")
 
+    def time_stage(self, X: torch.Tensor, stage: int, reps: int) -> float:
+        """Average duration (ms) of ``reps`` back-to-back launches of one kernel
+        (0 cross_root, 1 posterior_cov, 2 envelope), HIP events on the launch stream."""
+        X = X.detach().to(self.device, torch.double).contiguous()
+        kg = torch.empty(X.shape[0], dtype=torch.double, device=self.device)
+        ms = _lib.c_float()
+        _lib.check(_lib.load().dkg_plan_time_stage(self.host, self._dev_ptr, _lib.ptr(X), X.shape[0], _lib.ptr(kg),
+                                                   None, current_stream_ptr(self.device), stage, reps,
+                                                   ctypes.byref(ms)), "dkg_plan_time_stage")
+        return ms.value
+
     def forward(self, X: torch.Tensor, kg_pairs=None, timed: bool = False):
         X = X.detach().to(self.device, torch.double).contiguous()
         B = X.shape[0]

@@ -141,6 +141,12 @@ int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* 
 /* As dkg_plan_forward with per-kernel HIP-event timings (synchronises): stage_ms[3]. */
 int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                            double* kg_pairs, void* stream, float* stage_ms);
+/* Benchmark helper: average HIP-event duration (ms) of `reps` back-to-back
+ * launches of one stage (0 cross_root, 1 posterior_cov, 2 envelope) on
+ * `stream`, after one full forward that primes its inputs; a final full
+ * forward leaves kg / kg_pairs valid.  Synchronises. */
+int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                        double* kg_pairs, void* stream, int stage, int reps, float* avg_ms);
 
 /* Envelope stage alone: for P independent sets of L lines a_k + b_k z
  * (device, row-major [P][L]) kg[p] = E[max_k (a_k + b_k Z)] - max_k a_k, Z ~ N(0,1),
@@ -156,7 +162,7 @@ int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, d
 int dkg_debug_read_stamps(unsigned long long* host, int n);
 
 /* Debug/self-test of the register-only wave butterflies the kernels use
- * (DPP + v_permlane16/32_swap): in[64] -> out[512]; out[64 s + l] is the
+ * (DPP row ops + ds_bpermute for the 16/32 steps): in[64] -> out[512]; out[64 s + l] is the
  * partner value lane l receives at butterfly step s (0..5), out[384 + l] the
  * wave sum and out[448 + l] the wave max seen by lane l. */
 int dkg_debug_wave_ops(const double* in, double* out, void* stream);

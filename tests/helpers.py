@@ -69,3 +69,21 @@ def assert_kg_close(got: torch.Tensor, ref: torch.Tensor, floor: torch.Tensor, r
         f"{int(bad.sum())}/{bad.numel()} KG values outside rtol={rtol}+floor: "
         f"max err/tol={float((err / tol).max()):.3g}; worst got={got[bad][:4].tolist()} ref={ref[bad][:4].tolist()}")
     return float((err / tol).max())
+
+
+def load_golden(name: str):
+    """tests/golden/<name>.npz -> (state, oracle ModelList, D, W, X, arrays dict)."""
+    import os
+
+    import numpy as np
+
+    from dkg_amd.model import ModelListGPState, SingleTaskGPState
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{name}.npz")
+    z = dict(np.load(path))
+    t = {k: torch.from_numpy(v) for k, v in z.items()}
+    state = ModelListGPState(*[
+        SingleTaskGPState(t["train_x"], t["train_y"][:, i], t["lengthscale"][i], float(t["outputscale"][i]),
+                          float(t["noise"][i]), float(t["mean_constant"][i]))
+        for i in range(t["train_y"].shape[1])])
+    return state, to_oracle(state), t["D"], t["W"], t["X"], t

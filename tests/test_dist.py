@@ -1,0 +1,70 @@
+"""Sharded Discrete KG over 2 ranks (gloo, CPU) vs the unsharded oracle.
+
+SURVEY.md §8(e): the (candidate x scalarisation) pairs are split across ranks
+and combined with one collective (all-reduce over scalarisations, or
+all-gather over candidates).  Each rank's local evaluation is the oracle
+(injected), so this checks the partitioning and the exchange, not the kernels.
+Tolerance: the suite's KG tolerance (tests/helpers.py: 1e-6 relative plus the
+fp64 cancellation floor) — the oracle's batched matmuls round differently for
+a candidate slice than for the whole batch, at the 1e-14 absolute level.
+"""
+
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from dkg_amd.dist import shard_range
+from dkg_amd.synthetic import WORKLOADS, make_problem
+from helpers import assert_kg_close, rounding_floor, to_oracle
+from oracle.discretekg import discrete_kg_batched
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(tmp_path, axis, B, S, target):
+    out = str(tmp_path / f"{axis}_{B}_{S}.pt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "dist_worker.py"),
+           axis, str(B), str(S), str(-1 if target is None else target), out]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return torch.load(out, weights_only=True)
+
+
+def test_shard_range_covers():
+    for total in (0, 1, 3, 16, 17):
+        for world in (1, 2, 3, 8):
+            got = [shard_range(total, r, world) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+
+
+@pytest.mark.parametrize("axis,B,S,target", [
+    ("scalarisations", 8, 8, None),
+    ("scalarisations", 5, 3, 1),
+    ("scalarisations", 4, 1, None),   # S < world: rank 1 holds no scalarisation
+    ("candidates", 8, 8, None),
+    ("candidates", 5, 8, 0),          # ragged candidate split
+])
+def test_sharded_matches_unsharded(tmp_path, axis, B, S, target):
+    res = _launch(tmp_path, axis, B, S, target)
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    om = to_oracle(model)
+    ref = discrete_kg_batched(om, X[:B], D, W[:S], target)[0]
+    assert_kg_close(res["kg"], ref, rounding_floor(om, X[:B], D, W[:S], target))
+    calls = res["calls"]
+    if axis == "scalarisations":
+        assert sum(c[0][1] for c in calls if c) == S and all(c[0][0] == B for c in calls if c)
+    else:
+        assert sum(c[0][0] for c in calls if c) == B and all(c[0][1] == S for c in calls if c)

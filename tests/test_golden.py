@@ -1,0 +1,68 @@
+"""Golden vectors from the reference's own GP-problem fixtures (tests/golden/make_golden.py).
+
+CPU: the oracle still reproduces the committed vectors (guards the restatement
+against drift) and its batched form agrees with its per-candidate form.
+GPU: the HIP path through the C ABI matches them within the suite tolerance
+(1e-6 relative + the fp64 cancellation floor, tests/helpers.py).
+"""
+
+import pytest
+import torch
+
+from helpers import assert_kg_close, load_golden, rounding_floor
+from oracle.discretekg import (calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output,
+                               discrete_kg_batched, kg_pairs_from_lines, lines_batched)
+
+NAMES = ["lengthscales0", "observationnoise0"]
+PATHS = [("full", None), ("t0", 0), ("t1", 1)]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_reproduces_golden(name):
+    _, om, D, W, X, t = load_golden(name)
+    for i in (0, 5, 17):
+        torch.testing.assert_close(calculate_discrete_kg(om, X[i], D, W), t["kg_full"][i], rtol=1e-12, atol=1e-15)
+        torch.testing.assert_close(calculate_discrete_kg_conditioning_on_single_output(om, X[i], 1, D, W),
+                                   t["kg_t1"][i], rtol=1e-12, atol=1e-15)
+    a, b = lines_batched(om, X[:4], D, W, None)
+    torch.testing.assert_close(a, t["lines_a"], rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(b, t["lines_b"], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("key,target", PATHS)
+def test_batched_oracle_matches_golden(name, key, target):
+    _, om, D, W, X, t = load_golden(name)
+    kg, _ = discrete_kg_batched(om, X, D, W, target)
+    assert_kg_close(kg, t[f"kg_{key}"], rounding_floor(om, X, D, W, target))
+
+
+def test_golden_covers_short_circuit_and_positive():
+    for name in NAMES:
+        t = load_golden(name)[5]
+        assert (t["kg_full"] == 0).any() and (t["kg_full"] > 1e-4).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("key,target", PATHS)
+def test_native_matches_golden(name, key, target):
+    from dkg_amd import DiscreteKnowledgeGradient
+
+    state, om, D, W, X, t = load_golden(name)
+    acq = DiscreteKnowledgeGradient(state, D, W, target_output_ix=target, device="cuda:0")
+    kg = acq(X.unsqueeze(-2).cuda()).cpu()
+    assert_kg_close(kg, t[f"kg_{key}"], rounding_floor(om, X, D, W, target))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_native_lines_kg_matches_golden(name):
+    from dkg_amd import kg_from_lines
+
+    t = load_golden(name)[5]
+    a, b = t["lines_a"], t["lines_b"]
+    ref = kg_pairs_from_lines(a, b)
+    got = kg_from_lines(a.cuda(), b.cuda()).cpu()
+    floor = 64 * torch.finfo(torch.double).eps * a.abs().amax(-1)
+    assert_kg_close(got, ref, floor)

@@ -37,17 +37,28 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--collect", action="store_true",
+                    help="only aggregate gpurun_out/pmc_<tag> (merged back from the box) into profiles/")
     args = ap.parse_args()
     out = os.path.join(REPO, "gpurun_out", f"pmc_{args.tag}")
     os.makedirs(out, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     bench = [sys.executable, "bench.py", "--steps", str(args.steps), "--warmup", "5", "--cpu-seconds", "0",
              "--profile-reps", "2"]
+    if not args.collect:
+        profile(out, env, bench)
+    collect(args, out)
+
+
+def profile(out, env, bench):
     run(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", f"{out}/trace", "-o", "run", "--"]
         + bench, env)
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         run(["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", f"{out}/{ctr}", "-o", "run", "--"] + bench,
             env)
+
+
+def collect(args, out):
     agg = {}
     raw_rows = []
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
