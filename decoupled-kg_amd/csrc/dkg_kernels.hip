@@ -361,23 +361,28 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
   })
   const double bL = bmin, bR = bmax, aT = amax;
 
-  // ---- survivors: lines strictly above the chords L-T (b < bT) or T-R (b > bT)
-  //      h = (a - a0)(b1 - b0) - (a1 - a0)(b - b0) > 0, as a*db - b*da > a0*db - b0*da
+  // ---- survivors: lines strictly above the chord L-T or the chord T-R.
+  // No left/right select is needed: every line has a <= aT, so a line left of
+  // T is never above the extension of T-R (its slope is <= 0) and a line right
+  // of T never above the extension of L-T (slope >= 0); a degenerate chord
+  // (db = 0) admits nothing.  h = (a - a0) db - (b - b0) da > 0, evaluated as
+  // a*db - b*da > a0*db - b0*da.  Rounding can only admit extra lines (L, T
+  // or R themselves), which the exact test below discards.
   const double db1 = bT - bL, da1 = aT - aL, k1 = aL * db1 - bL * da1;
   const double db2 = bR - bT, da2 = aR - aT, k2 = aT * db2 - bT * da2;
   int cnt = 0;
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
     const double a = la[t], bb = lb[t];
-    const bool left = bb < bT;
-    const double db = left ? db1 : db2, da = left ? da1 : da2, kk = left ? k1 : k2;
-    const bool s = bb != bT && db > 0.0 && fma(a, db, -bb * da) > kk;
-    const uint64_t mask = __ballot(s);
-    if (s) {
-      const int pos = cnt + lanes_below(mask);
-      if (pos < ENV_CAP) { sb[pos] = bb; sa[pos] = a; }
+    const bool s = fma(a, db1, -bb * da1) > k1 || fma(a, db2, -bb * da2) > k2;
+    const uint64_t mk = __ballot(s);
+    if (mk != 0) {  // wave-uniform, rarely taken
+      if (s) {
+        const int pos = cnt + lanes_below(mk);
+        if (pos < ENV_CAP) { sb[pos] = bb; sa[pos] = a; }
+      }
+      cnt += __popcll(mk);
     }
-    cnt += __popcll(mask);
   }
   if (cnt + 3 > ENV_CAP) return envelope_walk<MAXL>(la, lb, nl, lane, bL, aL, bR, bT, nhull);
   if (lane == 0) {
@@ -390,52 +395,57 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  // ---- every candidate P decides on its own whether it is an envelope line:
-  // P is the max exactly on (cL, cR) with cR = min_{bQ > bP} (aP - aQ)/(bQ - bP)
-  // and cL = max_{bQ < bP} (aQ - aP)/(bP - bQ); it is on the envelope iff
-  // cL < cR and no other candidate has the same slope and a larger intercept
-  // (identical lines: the lowest index keeps it).  Each envelope line other
-  // than R contributes its right edge (P -> argmin Q):
-  //   (bQ - bP) psi(+-cR), minus sign when the edge ends at or left of T.
-  double v = 0.0;
-  int onenv = 0;
-  for (int e = lane; e < nc + 63 - ((nc + 63) % 64) && e < ENV_CAP; e += 64) {
+  // ---- right neighbour of every candidate P (one per lane, two chunks of 64
+  // at most): the line that takes over from P as z grows, i.e. the reference
+  // walk's step (discretekg.py:382-401): argmin over b_Q > b_P of the
+  // intersection (a_P - a_Q)/(b_Q - b_P), ties -> larger slope.  Compared by
+  // cross multiplication (both denominators > 0).
+  int nxt[2] = {-1, -1};
+  double cn[2] = {0.0, 0.0}, cd[2] = {1.0, 1.0}, cb[2] = {0.0, 0.0}, pb[2] = {0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c * 64 >= nc) break;
+    const int e = c * 64 + lane;
     const bool mine = e < nc;
     const double bP = mine ? sb[e] : 0.0, aP = mine ? sa[e] : 0.0;
-    double rn = INFINITY, rd = 1.0, rb = INFINITY;  // right: min (aP - aQ)/(bQ - bP); rb = bQ of the argmin
-    double ln = -INFINITY, ld = 1.0;                // left: max (aQ - aP)/(bP - bQ)
-    bool dominated = false;
+    double rn = 0.0, rd = 1.0, rb = 0.0;
+    int rj = -1;
 #pragma unroll 4
     for (int j = 0; j < nc; ++j) {
       const double bQ = sb[j], aQ = sa[j];
-      // right neighbour candidate: (aP - aQ)/(bQ - bP) over bQ > bP, argmin, ties -> larger bQ
       const double num = aP - aQ, den = bQ - bP;
       const double x = num * rd, y = rn * den;
-      const bool right = bQ > bP && (rb == INFINITY || x < y || (x == y && bQ > rb));
-      rn = right ? num : rn;
-      rd = right ? den : rd;
-      rb = right ? bQ : rb;
-      // left: max (aQ - aP)/(bP - bQ) over bQ < bP
-      const double lnum = aQ - aP, lden = bP - bQ;
-      const bool left = bQ < bP && (ln == -INFINITY || lnum * ld > ln * lden);
-      ln = left ? lnum : ln;
-      ld = left ? lden : ld;
-      dominated = dominated || (bQ == bP && (aQ > aP || (aQ == aP && j < e)));
+      const bool take = den > 0.0 && (rj < 0 || x < y || (x == y && bQ > rb));
+      rn = take ? num : rn;
+      rd = take ? den : rd;
+      rb = take ? bQ : rb;
+      rj = take ? j : rj;
     }
-    // cL < cR  <=>  ln/ld < rn/rd (both denominators > 0; infinities bracket L and R)
-    const bool env = mine && !dominated && (ln == -INFINITY || rb == INFINITY || ln * rd < rn * ld);
-    if (env && rb != INFINITY) {
-      const double c = rn / rd;
-      v += (rb - bP) * psi((rb <= bT) ? -c : c);
+    nxt[c] = rj; cn[c] = rn; cd[c] = rd; cb[c] = rb; pb[c] = bP;
+  }
+
+  // ---- follow the chain from L (index cnt): its members are the envelope
+  // lines in increasing slope, ending at R (no right neighbour).
+  uint64_t on0 = 0, on1 = 0;
+  int h = 0;
+  for (int cur = cnt, guard = 0; cur >= 0 && guard < nc; ++guard) {
+    if (cur < 64) on0 |= 1ull << cur; else on1 |= 1ull << (cur - 64);
+    ++h;
+    cur = (cur < 64) ? __builtin_amdgcn_readlane(nxt[0], cur) : __builtin_amdgcn_readlane(nxt[1], cur - 64);
+  }
+  // ---- each envelope line other than R contributes its right edge P -> Q:
+  //   (b_Q - b_P) psi(+-c), minus sign when the edge ends at or left of T.
+  double v = 0.0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c * 64 >= nc) break;
+    const bool on = (((c == 0) ? on0 : on1) >> lane) & 1;
+    if (on && nxt[c] >= 0) {
+      const double cc = cn[c] / cd[c];
+      v += (cb[c] - pb[c]) * psi((cb[c] <= bT) ? -cc : cc);
     }
-    onenv += env ? 1 : 0;
   }
-  if (nhull) {
-    int hsum = onenv;
-    hsum += __shfl_xor(hsum, 1); hsum += __shfl_xor(hsum, 2); hsum += __shfl_xor(hsum, 4);
-    hsum += __shfl_xor(hsum, 8); hsum += __shfl_xor(hsum, 16); hsum += __shfl_xor(hsum, 32);
-    *nhull = hsum;
-  }
+  if (nhull) *nhull = h;
   return wave_sum(v);
 }
 
@@ -512,7 +522,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   // ---- one round of memory traffic: DMA the line data, plain loads for the rest
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    if (i < m) {
+    if (i < m && !(dbg & 8)) {
       dma_to_lds(P->o[i].disc_mean, lmu + (size_t)i * SLp, N, wave, SW, lane);
       if (full || i == target) dma_to_lds(P->cov[i] + (size_t)b * N, lcv + (size_t)i * SLp, N, wave, SW, lane);
     }
@@ -587,7 +597,13 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
 #pragma unroll
     for (int i = 0; i < M; ++i) mup[i] = lmu + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
     double la[MAXL], lb[MAXL];
-    if (full) {
+    if (dbg & 16) {  // ablation: no line build (synthetic lines)
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) {
+        la[t] = a_off * (double)(lane + t);
+        lb[t] = wb[0] * (double)(lane - t);
+      }
+    } else if (full) {
       const double* cvp[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) cvp[i] = lcv + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
