@@ -34,6 +34,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct WsLayout {
   size_t q[DKG_MAX_OUTPUTS];
   size_t mux[DKG_MAX_OUTPUTS];
+  size_t var[DKG_MAX_OUTPUTS];
   size_t cov[DKG_MAX_OUTPUTS];
   size_t wg_part;
   size_t tickets;
@@ -48,6 +49,8 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S) {
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
     L.mux[i] = off;
+    off = align256(off + Bp * sizeof(double));
+    L.var[i] = off;
     off = align256(off + Bp * sizeof(double));
     L.cov[i] = off;
     off = align256(off + (size_t)std::max(B, 1) * std::max(N, 1) * sizeof(double));
@@ -116,6 +119,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
     P->max_np = std::max(P->max_np, pad16(outs[i].n));
     P->q[i] = reinterpret_cast<double*>(ws + L.q[i]);
     P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
+    P->var[i] = reinterpret_cast<double*>(ws + L.var[i]);
     P->cov[i] = reinterpret_cast<double*>(ws + L.cov[i]);
   }
   P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
@@ -124,6 +128,8 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
   P->debug_env = denv ? std::atoi(denv) : 0;
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
+  static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
+  P->debug_stamp = dst ? std::atoi(dst) : 0;
   return DKG_OK;
 }
 
@@ -297,6 +303,10 @@ int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, d
   if (L > 64 * 33) return fail(DKG_ERR_UNSUPPORTED, "L=%d lines per set (supported <= %d)", L, 64 * 33);
   if (!intercepts || !slopes || !kg) return fail(DKG_ERR_ARG, "NULL pointer");
   return hip_check(launch_lines_kg(intercepts, slopes, P, L, kg, n_hull, (hipStream_t)stream), "lines_kg_kernel");
+}
+
+int dkg_debug_read_kstamps(unsigned long long* host, int n) {
+  return hip_check(read_kstamps(host, n), "hipMemcpyFromSymbol");
 }
 
 int dkg_debug_read_stamps(unsigned long long* host, int n) {

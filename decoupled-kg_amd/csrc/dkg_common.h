@@ -41,6 +41,22 @@ __device__ __forceinline__ double kernel_profile(int kind, double r2) {
   return (t + 1.0 + (5.0 / 3.0) * r2) * exp(-t);
 }
 
+// Same with the family fixed at compile time (branch-free in unrolled loops).
+template <int KIND>
+__device__ __forceinline__ double kernel_profile_t(double r2) {
+  if constexpr (KIND == DKG_RBF) {
+    return exp(-0.5 * r2);
+  } else if constexpr (KIND == DKG_MATERN12) {
+    return exp(-sqrt(r2));
+  } else if constexpr (KIND == DKG_MATERN32) {
+    const double t = 1.7320508075688772 * sqrt(r2);
+    return (t + 1.0) * exp(-t);
+  } else {
+    const double t = 2.23606797749979 * sqrt(r2);
+    return (t + 1.0 + (5.0 / 3.0) * r2) * exp(-t);
+  }
+}
+
 __device__ __forceinline__ double scaled_r2(const double* __restrict__ xa, const double* __restrict__ xb,
                                             const double* __restrict__ il, int d) {
   double acc = 0.0;
@@ -51,19 +67,23 @@ __device__ __forceinline__ double scaled_r2(const double* __restrict__ xa, const
   return acc;
 }
 
-// Same with the first point held in registers (d <= DKG_MAX_DIM, unrolled).
-__device__ __forceinline__ double scaled_r2_reg(const double (&xa)[DKG_MAX_DIM], const double* __restrict__ xb,
-                                                const double* __restrict__ il, int d) {
+// Compile-time bound DM >= d: unrolled, branch-free, every load issued up
+// front (indices clamped to d - 1; terms k >= d contribute zero).
+template <int DM>
+__device__ __forceinline__ double scaled_r2_dm(const double* __restrict__ xa, const double* __restrict__ xb,
+                                               const double* __restrict__ il, int d) {
   double acc = 0.0;
 #pragma unroll
-  for (int k = 0; k < DKG_MAX_DIM; ++k) {
-    if (k < d) {
-      const double t = (xa[k] - xb[k]) * il[k];
-      acc = fma(t, t, acc);
-    }
+  for (int k = 0; k < DM; ++k) {
+    const int kk = min(k, d - 1);
+    const double t = (xa[kk] - xb[kk]) * il[kk];
+    acc = fma(t, (k < d) ? t : 0.0, acc);
   }
   return acc;
 }
+
+// Dimension bucket used to instantiate the kernels: 2, 4, 8 or 16.
+__host__ __device__ inline int dim_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
 // ---------------------------------------------------------------------------
 // Wave butterflies: DPP within 16-lane rows (xor 1, xor 2 via quad_perm;

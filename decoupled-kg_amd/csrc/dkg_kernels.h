@@ -15,11 +15,12 @@ struct Plan {
   int32_t max_B, max_np;            // workspace sized for max_B candidates; max n_pad over outputs
   int32_t sw, split;                // envelope geometry: waves per workgroup, workgroups per candidate
   int32_t debug_env, debug_cov;     // ablation switches (0 in production)
-  int32_t pad_;
+  int32_t debug_stamp;              // 1: per-workgroup phase stamps into g_kstamps (0 in production)
   const double* disc;               // [N x d]
   const double* weights;            // [S x m]
   double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
   double* mux[DKG_MAX_OUTPUTS];     // posterior mean at the candidates per output (workspace)
+  double* var[DKG_MAX_OUTPUTS];     // noiseless posterior variance s - |Q_X[b]|^2 per output (workspace)
   double* cov[DKG_MAX_OUTPUTS];     // [B x N] posterior covariance rows per output (workspace)
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
   int* tickets;                     // [B] arrival counters (split > 2 only)
@@ -45,6 +46,9 @@ hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew,
                           hipStream_t s, hipEvent_t* ev);
 hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s);
 hipError_t read_stamps(unsigned long long* host, int n);
+// Per-workgroup phase stamps of the forward kernels: [3 kernels][KST_WG][8].
+constexpr int KST_WG = 1024;
+hipError_t read_kstamps(unsigned long long* host, int n);
 hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s);
 hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStream_t s);
 

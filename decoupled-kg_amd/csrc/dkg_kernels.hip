@@ -8,6 +8,8 @@
 #include "dkg_common.h"
 #include "dkg_kernels.h"
 
+#include <type_traits>
+
 namespace dkg {
 
 // ---------------------------------------------------------------------------
@@ -49,12 +51,39 @@ __global__ void pack_root_kernel(const double* __restrict__ r, int n, double* __
 // LDS in B-operand order, and the k range is split over the 8 waves
 // (split-K) with every operand of a wave's chunk loaded before its MFMAs;
 // partials are reduced in LDS in fixed wave order (deterministic).
+// Per-workgroup phase stamps (Plan.debug_stamp): slot 0 = s_memrealtime at
+// start (100 MHz), 1..6 = s_memtime at phase boundaries, 7 = s_memrealtime at end.
+__device__ unsigned long long g_kstamps[3 * KST_WG * 8];
+__device__ __forceinline__ unsigned long long* kst_slot(int debug, int kid) {
+  const int wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  return (debug && threadIdx.x == 0 && wg < KST_WG) ? g_kstamps + ((size_t)kid * KST_WG + wg) * 8 : nullptr;
+}
+#define KST_BEGIN(st)                                                  \
+  do {                                                                 \
+    if (st) {                                                          \
+      (st)[0] = __builtin_amdgcn_s_memrealtime();                      \
+      (st)[1] = __builtin_amdgcn_s_memtime();                          \
+    }                                                                  \
+  } while (0)
+#define KST(st, k)                                                     \
+  do {                                                                 \
+    if (st) (st)[k] = __builtin_amdgcn_s_memtime();                    \
+  } while (0)
+#define KST_END(st)                                                    \
+  do {                                                                 \
+    if (st) {                                                          \
+      (st)[6] = __builtin_amdgcn_s_memtime();                          \
+      (st)[7] = __builtin_amdgcn_s_memrealtime();                      \
+    }                                                                  \
+  } while (0)
+
 constexpr int CR_WAVES = 8;
 constexpr int CR_U = 8;  // k-blocks per load batch
 
+template <int DM>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
                                                 double* __restrict__ qout, double* __restrict__ mout, int ti, int p,
-                                                double* smem) {
+                                                double* smem, unsigned long long* st = nullptr) {
   const int n = o.n;
   const int np = pad16(n);
   const int T = np / 16;
@@ -74,46 +103,92 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   double* xs = mred + CR_WAVES * 16;             // [np][d] staged training inputs
   double* als = xs + (size_t)np * d;             // [np] alpha
 
-  const bool want_mean = (mout != nullptr) && (p == 0);  // p == 0 covers every column
-  for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e];
-  if (want_mean)
-    for (int e = tid; e < ncol; e += CR_WAVES * WAVE) als[e] = o.alpha[e];
-  const int row = ti * 16 + (lane & 15);
-  const bool rv = row < rows;
-  double xr[DKG_MAX_DIM];
-#pragma unroll
-  for (int k = 0; k < DKG_MAX_DIM; ++k) xr[k] = (rv && k < d) ? x[(size_t)row * d + k] : 0.0;
-  __syncthreads();
-
-  // ---- fill K(x_row, X_col), col < 4*kbB, in B-operand order (zero outside)
-  double mpart = 0.0;
-  for (int e = tid; e < kbB * 64; e += CR_WAVES * WAVE) {
-    const int col = 4 * (e >> 6) + (lane >> 4);
-    double v = 0.0;
-    if (rv && col < n) {
-      v = o.outputscale * kernel_profile(o.kernel, scaled_r2_reg(xr, xs + (size_t)col * d, o.inv_lengthscale, d));
-      if (want_mean) mpart = fma(v, als[col], mpart);
-    }
-    kb_lds[e] = v;
-  }
-  __syncthreads();
-
-  // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
+  // R fragments of this wave's first k-block batch: loaded before anything
+  // else so their latency overlaps the staging and the kernel evaluations.
   const double* rfA = o.root_frag + (size_t)tA * KB * 64 + lane;
   const double* rfB = o.root_frag + (size_t)tB * KB * 64 + lane;
   const int chunk = (kbB + CR_WAVES - 1) / CR_WAVES;
   const int k0 = wave * chunk;
   const int k1 = min(kbB, k0 + chunk);
+  double ra[CR_U], rb[CR_U];
+#pragma unroll
+  for (int u = 0; u < CR_U; ++u) {
+    const int kb = min(k0 + u, kbB - 1);
+    rb[u] = rfB[(size_t)kb * 64];
+    ra[u] = rfA[(size_t)min(kb, kbA - 1) * 64];
+  }
+
+  KST(st, 2);
+  const bool want_mean = (mout != nullptr) && (p == 0);  // p == 0 covers every column
+  // training inputs staged pre-scaled by 1/lengthscale (GPyTorch divides both
+  // inputs by the lengthscale before the distance)
+  for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e] * o.inv_lengthscale[e % d];
+  if (want_mean)
+    for (int e = tid; e < ncol; e += CR_WAVES * WAVE) als[e] = o.alpha[e];
+  const int row = ti * 16 + (lane & 15);
+  const bool rv = row < rows;
+  const int rowc = min(row, rows - 1);
+  double xr[DM];  // the candidate row, pre-scaled (clamped loads, no branches)
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    const int kk = min(k, d - 1);
+    xr[k] = x[(size_t)rowc * d + kk] * o.inv_lengthscale[kk];
+  }
+  __syncthreads();
+
+  KST(st, 3);
+  // ---- fill K(x_row, X_col), col < 4*kbB, in B-operand order (zero outside)
+  double mpart = 0.0;
+  const double os = o.outputscale;
+  const int fill = kbB * 64;
+  const int iters = (fill + CR_WAVES * WAVE - 1) / (CR_WAVES * WAVE);  // uniform trip count
+  // one straight-line loop per covariance family (the switch stays outside)
+  auto fill_loop = [&](auto kind_c) {
+    constexpr int KIND = decltype(kind_c)::value;
+#pragma unroll 4
+    for (int it = 0; it < iters; ++it) {
+      const int e = tid + it * CR_WAVES * WAVE;
+      const int col = 4 * (e >> 6) + (lane >> 4);
+      const int cc = min(col, n - 1);
+      double r2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < DM; ++k) {
+        const double t = xr[k] - xs[(size_t)cc * d + min(k, d - 1)];
+        r2 = fma(t, (k < d) ? t : 0.0, r2);
+      }
+      const double kv = os * kernel_profile_t<KIND>(r2);
+      const double v = (rv && col < n) ? kv : 0.0;
+      const double al = als[cc];  // staged only when want_mean; otherwise ignored
+      mpart = fma(v, want_mean ? al : 0.0, mpart);
+      if (e < fill) kb_lds[e] = v;
+    }
+  };
+  switch (o.kernel) {
+    case DKG_MATERN12: fill_loop(std::integral_constant<int, DKG_MATERN12>{}); break;
+    case DKG_MATERN32: fill_loop(std::integral_constant<int, DKG_MATERN32>{}); break;
+    case DKG_RBF: fill_loop(std::integral_constant<int, DKG_RBF>{}); break;
+    default: fill_loop(std::integral_constant<int, DKG_MATERN52>{}); break;
+  }
+  __syncthreads();
+
+  KST(st, 4);
+  // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
   d4 accA2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
   d4 accB2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
   const bool pairA = tA != tB;
   for (int base = k0; base < k1; base += CR_U) {
-    double ra[CR_U], rb[CR_U], bo[CR_U];
+    double bo[CR_U];
+    if (base != k0) {
+#pragma unroll
+      for (int u = 0; u < CR_U; ++u) {
+        const int kb = min(base + u, kbB - 1);
+        rb[u] = rfB[(size_t)kb * 64];
+        ra[u] = rfA[(size_t)min(kb, kbA - 1) * 64];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < CR_U; ++u) {
       const int kb = min(base + u, kbB - 1);
-      rb[u] = rfB[(size_t)kb * 64];
-      ra[u] = rfA[(size_t)min(kb, kbA - 1) * 64];
       bo[u] = (base + u < k1) ? kb_lds[kb * 64 + lane] : 0.0;
     }
 #pragma unroll
@@ -137,6 +212,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   }
   __syncthreads();
 
+  KST(st, 5);
   // ---- reduce partials in fixed wave order; wave w finalises (tile, reg) = w.
   {
     const int tsel = wave >> 2;  // 0 -> tA, 1 -> tB
@@ -157,19 +233,24 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
     const int rr = ti * 16 + tid;
     mout[rr] = (rr < rows) ? o.mean_constant + s : 0.0;
   }
+  KST_END(st);
 }
 
+template <int DM>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  cross_root_impl(a.o, a.d, a.x, a.rows, a.q, a.mean, blockIdx.x, blockIdx.y, smem);
+  cross_root_impl<DM>(a.o, a.d, a.x, a.rows, a.q, a.mean, blockIdx.x, blockIdx.y, smem);
 }
 
 // Forward: grid (B tiles, pairs, outputs); workgroup (0,0,0) also clears the
 // KG accumulators (and arrival tickets) the envelope stage adds into.
+template <int DM>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const Plan* __restrict__ P,
                                                                           const double* __restrict__ xnew, int B,
                                                                           double* __restrict__ kg) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  unsigned long long* st = kst_slot(P->debug_stamp, 0);
+  KST_BEGIN(st);
   const int oi = blockIdx.z;
   if (blockIdx.x == 0 && blockIdx.y == 0 && oi == 0) {
     for (int i = threadIdx.x; i < B; i += blockDim.x) {
@@ -177,7 +258,7 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
       if (P->split > 2) P->tickets[i] = 0;
     }
   }
-  cross_root_impl(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem);
+  cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
 }
 
 size_t cross_root_lds_bytes(int np, int d) {
@@ -194,16 +275,22 @@ size_t cross_root_lds_bytes(int np, int d) {
 constexpr int PC_WAVES = 4;
 constexpr int PC_U = 16;
 
-__global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
+// 4 workgroups per CU (<= 128 VGPRs): the whole 1024-workgroup headline grid is resident at once.
+template <int DM>
+__global__ __launch_bounds__(PC_WAVES * WAVE, 4) void posterior_cov_kernel(const Plan* __restrict__ P,
                                                                          const double* __restrict__ xnew, int B) {
   __shared__ __attribute__((aligned(16))) double part[PC_WAVES * 4 * 64];
+  __shared__ double qpart[PC_WAVES * 16];
+  unsigned long long* st = kst_slot(P->debug_stamp, 1);
+  KST_BEGIN(st);
   const int tk = blockIdx.x;
   const int ti = blockIdx.y;
   const int oi = blockIdx.z;
   const dkg_output& o = P->o[oi];
   const int N = P->N;
   const int dbg = P->debug_cov;
-  if (tk * 16 >= N) return;
+  if (tk > 0 && tk * 16 >= N) return;  // tile 0 always runs: it also produces the candidates' variances
+  const bool have_d = N > 0;
   const int KB = pad16(o.n) / 4;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -215,7 +302,17 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   const double* qd = o.disc_frag + (size_t)tk * KB * 64 + lane;
   // four independent accumulation chains (k-block mod 4): the f64 MFMA
   // dependent-issue latency is hidden by the other chains
+  // epilogue operands (row b, column k of register r = wave) first: their
+  // latency overlaps the fragment loads
+  const int b = ti * 16 + (lane >> 4) + 4 * wave;
+  const int k = tk * 16 + (lane & 15);
+  const int d = P->d;
+  const double* xb = xnew + (size_t)min(b, B - 1) * d;
+  const double* xk = have_d ? P->disc + (size_t)min(k, N - 1) * d : xb;
+  const double r2 = scaled_r2_dm<DM>(xb, xk, o.inv_lengthscale, d);
+  KST(st, 2);
   d4 acc[4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  double qsq = 0.0;  // lane l: sum over this wave's k of Q_X[16 ti + (l & 15)][k]^2 (k = 4 kb + (l >> 4))
   for (int base = k0; base < k1; base += PC_U) {
     double ra[PC_U], rb[PC_U];
 #pragma unroll
@@ -226,7 +323,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
         rb[u] = 0.5;
       } else {
         ra[u] = qa[(size_t)kb * 64];
-        rb[u] = (base + u < k1) ? qd[(size_t)kb * 64] : 0.0;
+        rb[u] = (have_d && base + u < k1) ? qd[(size_t)kb * 64] : 0.0;
       }
     }
     if (dbg & 2) {
@@ -236,24 +333,36 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     }
 #pragma unroll
     for (int u = 0; u < PC_U; ++u) acc[u & 3] = mfma_f64(ra[u], rb[u], acc[u & 3]);
+    if (tk == 0) {  // the candidates' own |Q_X[b]|^2 (padding k-blocks of the batch repeat the last one)
+#pragma unroll
+      for (int u = 0; u < PC_U; ++u) qsq = (base + u < k1) ? fma(ra[u], ra[u], qsq) : qsq;
+    }
   }
   const d4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  // epilogue operands (row b, column k of register r = wave) fetched while partials land
-  const int b = ti * 16 + (lane >> 4) + 4 * wave;
-  const int k = tk * 16 + (lane & 15);
-  const int d = P->d;
-  const double* xb = xnew + (size_t)min(b, B - 1) * d;
-  const double* xk = P->disc + (size_t)min(k, N - 1) * d;
-  const double r2 = scaled_r2(xb, xk, o.inv_lengthscale, d);
+  KST(st, 3);
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[(wave * 4 + r) * 64 + lane] = accs[r];
+  if (tk == 0) {
+    qsq += __shfl_xor(qsq, 16);
+    qsq += __shfl_xor(qsq, 32);
+    if (lane < 16) qpart[wave * 16 + lane] = qsq;
+  }
   __syncthreads();
+  if (tk == 0 && threadIdx.x < 16) {
+    const int bb = ti * 16 + threadIdx.x;
+    double q2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < PC_WAVES; ++w) q2 += qpart[w * 16 + threadIdx.x];
+    if (bb < B) P->var[oi][bb] = o.outputscale - q2;
+  }
 
+  KST(st, 4);
   double s = 0.0;
 #pragma unroll
   for (int w = 0; w < PC_WAVES; ++w) s += part[(w * 4 + wave) * 64 + lane];
   if (b < B && k < N)
     P->cov[oi][(size_t)b * N + k] = ((dbg & 4) ? r2 : o.outputscale * kernel_profile(o.kernel, r2)) - s;
+  KST_END(st);
 }
 
 // ---------------------------------------------------------------------------
@@ -499,6 +608,8 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   const bool full = target < 0;
   const int SL = stage_len(N);
   DKG_STAMP(0);
+  unsigned long long* st = kst_slot(P->debug_stamp, 2);
+  KST_BEGIN(st);
 
   // Per-output scalars, hoisted once (static kernarg offsets).
   double ysd[M], ymu[M], nz[M], os[M];
@@ -528,34 +639,16 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     }
   }
   for (int e = threadIdx.x; e < S * m; e += blockDim.x) lw[e] = P->weights[e];
-  // candidate's own posterior: v_i = s_i - |Q_i[b]|^2 (wave i), mean from the cross stage
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    if (i < m && wave == i % SW) {
-      const int KB = pad16(P->o[i].n) / 4;
-      const double* q = P->q[i] + (size_t)(b >> 4) * KB * 64 + (b & 15);
-      double acc = 0.0;
-      for (int base = lane; base < KB * 4; base += 8 * 64) {
-        double vq[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = min(base + 64 * u, KB * 4 - 1);
-          vq[u] = (base + 64 * u < KB * 4) ? q[(size_t)(e >> 2) * 64 + 16 * (e & 3)] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = fma(vq[u], vq[u], acc);
-      }
-      const double mx = P->mux[i][b];
-      acc = wave_sum(acc);
-      if (lane == 0) {
-        s_sv[i] = os[i] - acc;
-        s_mx[i] = mx;
-      }
-    }
+  // candidate's own posterior (variance from the covariance stage, mean from the cross stage)
+  if (threadIdx.x < m) {
+    s_sv[threadIdx.x] = P->var[threadIdx.x][b];
+    s_mx[threadIdx.x] = P->mux[threadIdx.x][b];
   }
+  KST(st, 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   DKG_STAMP(1);
+  KST(st, 3);
 
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
   double* sa = sb + ENV_CAP;
@@ -668,9 +761,11 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
 
   // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
+  KST(st, 4);
   if (lane == 0) s_tail[wave] = wave_acc;
   __syncthreads();
   DKG_STAMP(4);
+  KST(st, 5);
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int w2 = 0; w2 < SW; ++w2) s += s_tail[w2];
@@ -698,6 +793,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
   __syncthreads();
   DKG_STAMP(5);
+  KST_END(st);
 }
 
 static int outputs_bucket(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 3 ? 3 : m <= 4 ? 4 : 8; }
@@ -777,12 +873,40 @@ hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s) {
+template <int DM>
+static hipError_t launch_cross_root_t(const CrossArgs& a, hipStream_t s) {
   const int np = pad16(a.o.n);
   dim3 grid(pad16(a.rows) / 16, (np / 16 + 1) / 2, 1);
   const size_t lds = cross_root_lds_bytes(np, a.d);
-  if (lds > 65536) (void)hipFuncSetAttribute((const void*)cross_root_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(cross_root_kernel, grid, dim3(CR_WAVES * WAVE), lds, s, a);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)cross_root_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(cross_root_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s) {
+  switch (dim_bucket(a.d)) {
+    case 2: return launch_cross_root_t<2>(a, s);
+    case 4: return launch_cross_root_t<4>(a, s);
+    case 8: return launch_cross_root_t<8>(a, s);
+    default: return launch_cross_root_t<16>(a, s);
+  }
+}
+
+template <int DM>
+static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
+                                     hipStream_t s, int stage) {
+  if (stage == 0) {
+    dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m);
+    const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+    hipLaunchKernelGGL(cross_root_plan_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg);
+    return hipGetLastError();
+  }
+  dim3 grid(std::max(1, pad16(h.N) / 16), pad16(B) / 16, h.m);
+  hipLaunchKernelGGL(posterior_cov_kernel<DM>, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B);
   return hipGetLastError();
 }
 
@@ -821,20 +945,13 @@ static hipError_t launch_env_m(int lines, const Plan* dev, int B, double* kg, do
 // recorded around them (dkg_forward_timed).
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                         hipStream_t s, int stage) {
-  if (stage == 0) {
-    dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m);
-    const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
-    if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
-    hipLaunchKernelGGL(cross_root_plan_kernel, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg);
-    return hipGetLastError();
-  }
-  if (stage == 1) {
-    if (h.N == 0) return hipSuccess;
-    dim3 grid(pad16(h.N) / 16, pad16(B) / 16, h.m);
-    hipLaunchKernelGGL(posterior_cov_kernel, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B);
-    return hipGetLastError();
+  if (stage == 0 || stage == 1) {
+    switch (dim_bucket(h.d)) {
+      case 2: return launch_cross_cov_t<2>(h, dev, xnew, B, kg, s, stage);
+      case 4: return launch_cross_cov_t<4>(h, dev, xnew, B, kg, s, stage);
+      case 8: return launch_cross_cov_t<8>(h, dev, xnew, B, kg, s, stage);
+      default: return launch_cross_cov_t<16>(h, dev, xnew, B, kg, s, stage);
+    }
   }
   dim3 grid(B, h.split), block(h.sw * WAVE);
   const size_t lds = envelope_lds_bytes(h.m, h.N, h.sw, h.S);
@@ -869,6 +986,10 @@ hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, doubl
   else if (L <= 64 * 33) hipLaunchKernelGGL(lines_kg_kernel<33>, grid, block, lds, s, a, b, P, L, kg, nhull);
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t read_kstamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kstamps), sizeof(unsigned long long) * std::min(n, 3 * KST_WG * 8));
 }
 
 hipError_t read_stamps(unsigned long long* host, int n) {

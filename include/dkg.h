@@ -160,6 +160,11 @@ int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, d
 /* Debug: copy the envelope kernel's phase stamps (written when the env var
  * DKG_DEBUG_ENV_FLAGS has bit 4 set at plan creation) to host memory: n words. */
 int dkg_debug_read_stamps(unsigned long long* host, int n);
+/* Debug: per-workgroup phase stamps of the three forward kernels, written when
+ * the env var DKG_DEBUG_STAMPS=1 at plan creation: [3][1024][8] words (slot 0
+ * s_memrealtime at start, 1..6 s_memtime at phase boundaries, 7 s_memrealtime
+ * at end); n words are copied. */
+int dkg_debug_read_kstamps(unsigned long long* host, int n);
 
 /* Debug/self-test of the register-only wave butterflies the kernels use
  * (DPP row ops + ds_bpermute for the 16/32 steps): in[64] -> out[512]; out[64 s + l] is the

@@ -66,3 +66,15 @@ def test_native_lines_kg_matches_golden(name):
     got = kg_from_lines(a.cuda(), b.cuda()).cpu()
     floor = 64 * torch.finfo(torch.double).eps * a.abs().amax(-1)
     assert_kg_close(got, ref, floor)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("target", [None, 1])
+def test_native_empty_discretisation(target):
+    """N = 0: only the candidate's own line, so KG = 0 (discretekg.py:182-235 with D empty)."""
+    from dkg_amd import DiscreteKnowledgeGradient
+
+    state, om, D, W, X, t = load_golden("lengthscales0")
+    acq = DiscreteKnowledgeGradient(state, D[:0], W, target_output_ix=target, device="cuda:0")
+    kg = acq(X[:5].unsqueeze(-2).cuda()).cpu()
+    assert torch.equal(kg, torch.zeros(5, dtype=torch.double))
