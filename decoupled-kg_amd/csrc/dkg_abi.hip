@@ -112,7 +112,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->max_np = 16;
   P->sw = sw;
   P->split = split;
-  P->disc = disc;
+  P->disc = (N > 0) ? disc : reinterpret_cast<const double*>(ws);  // always a readable address
   P->weights = weights;
   for (int i = 0; i < m; ++i) {
     P->o[i] = outs[i];

@@ -27,6 +27,19 @@ __device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// Pair-packed fragment layout (include/dkg.h "Data layout"): element
+// (row 16 t + (l & 15), column 4 kb + (l >> 4)) of a matrix with KB = n_pad/4
+// k-blocks sits at ((t * KB/2 + kb/2) * 64 + l) * 2 + (kb & 1), so lane l's
+// operands of k-blocks 2j and 2j+1 are one aligned 16-byte word.
+__host__ __device__ inline size_t frag_index(int t, int kb, int l, int KB) {
+  return (((size_t)t * (KB >> 1) + (kb >> 1)) * 64 + l) * 2 + (kb & 1);
+}
+
+// Lane's operands of k-blocks 2 j and 2 j + 1 of tile `tile` (base = matrix start).
+__device__ __forceinline__ double2 frag_pair(const double* __restrict__ base, int tile, int j, int lane, int KB) {
+  return reinterpret_cast<const double2*>(base)[((size_t)tile * (KB >> 1) + j) * 64 + lane];
+}
+
 // Kernel profile of ScaleKernel(base) at squared scaled distance r2:
 // gpytorch MaternKernel.forward / RBFKernel (factory.py:116 catalog).
 __device__ __forceinline__ double kernel_profile(int kind, double r2) {
@@ -135,6 +148,13 @@ __device__ __forceinline__ double wave_max(double v) {
 // A condition every lane agrees on, made visibly wave-uniform (scalar branch,
 // full EXEC) so cross-lane operations inside the branch see every lane.
 __device__ __forceinline__ bool uniform(bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; }
+
+// Lane `l`'s value of v (l wave-uniform), as a scalar operand.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
 
 __device__ __forceinline__ int lanes_below(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));

@@ -32,13 +32,14 @@ __global__ void pack_root_kernel(const double* __restrict__ r, int n, double* __
   const int KB = np / 4;
   const size_t total = (size_t)np * np;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    // e enumerates (tj, kb, l) of the R^T view; written at its pair-packed slot
     const int l = (int)(e & 63);
     const size_t blk = e >> 6;
     const int kb = (int)(blk % KB);
     const int tj = (int)(blk / KB);
     const int row = 4 * kb + (l >> 4);
     const int col = 16 * tj + (l & 15);
-    rf[e] = (row < n && col < n) ? r[(size_t)row * n + col] : 0.0;
+    rf[frag_index(tj, kb, l, KB)] = (row < n && col < n) ? r[(size_t)row * n + col] : 0.0;
   }
 }
 
@@ -105,17 +106,18 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
 
   // R fragments of this wave's first k-block batch: loaded before anything
   // else so their latency overlaps the staging and the kernel evaluations.
-  const double* rfA = o.root_frag + (size_t)tA * KB * 64 + lane;
-  const double* rfB = o.root_frag + (size_t)tB * KB * 64 + lane;
-  const int chunk = (kbB + CR_WAVES - 1) / CR_WAVES;
+  // (k-block ranges are even: kbA, kbB are multiples of 4 and chunk is even)
+  const int chunk = 2 * ((kbB / 2 + CR_WAVES - 1) / CR_WAVES);
   const int k0 = wave * chunk;
   const int k1 = min(kbB, k0 + chunk);
   double ra[CR_U], rb[CR_U];
 #pragma unroll
-  for (int u = 0; u < CR_U; ++u) {
-    const int kb = min(k0 + u, kbB - 1);
-    rb[u] = rfB[(size_t)kb * 64];
-    ra[u] = rfA[(size_t)min(kb, kbA - 1) * 64];
+  for (int u = 0; u < CR_U; u += 2) {
+    const int j = min(k0 + u, kbB - 2) >> 1;
+    const double2 vb = frag_pair(o.root_frag, tB, j, lane, KB);
+    const double2 va = frag_pair(o.root_frag, tA, min(j, kbA / 2 - 1), lane, KB);
+    rb[u] = vb.x; rb[u + 1] = vb.y;
+    ra[u] = va.x; ra[u + 1] = va.y;
   }
 
   KST(st, 2);
@@ -180,10 +182,12 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
     double bo[CR_U];
     if (base != k0) {
 #pragma unroll
-      for (int u = 0; u < CR_U; ++u) {
-        const int kb = min(base + u, kbB - 1);
-        rb[u] = rfB[(size_t)kb * 64];
-        ra[u] = rfA[(size_t)min(kb, kbA - 1) * 64];
+      for (int u = 0; u < CR_U; u += 2) {
+        const int j = min(base + u, kbB - 2) >> 1;
+        const double2 vb = frag_pair(o.root_frag, tB, j, lane, KB);
+        const double2 va = frag_pair(o.root_frag, tA, min(j, kbA / 2 - 1), lane, KB);
+        rb[u] = vb.x; rb[u + 1] = vb.y;
+        ra[u] = va.x; ra[u + 1] = va.y;
       }
     }
 #pragma unroll
@@ -223,7 +227,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       for (int w = 0; w < CR_WAVES; ++w) s += part[(w * 8 + tsel * 4 + r) * 64 + lane];
       const int tj = tsel ? tB : tA;
       // D = R^T K^T: lane holds Q[16ti + (l&15)][16tj + 4r + (l>>4)] = q_frag[ti][4tj + r][l]
-      qout[((size_t)ti * KB + 4 * tj + r) * 64 + lane] = s;
+      qout[frag_index(ti, 4 * tj + r, lane, KB)] = s;
     }
   }
   if (want_mean && tid < 16) {
@@ -247,9 +251,9 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a
 template <int DM>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const Plan* __restrict__ P,
                                                                           const double* __restrict__ xnew, int B,
-                                                                          double* __restrict__ kg) {
+                                                                          double* __restrict__ kg, int dst) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  unsigned long long* st = kst_slot(P->debug_stamp, 0);
+  unsigned long long* st = kst_slot(dst, 0);
   KST_BEGIN(st);
   const int oi = blockIdx.z;
   if (blockIdx.x == 0 && blockIdx.y == 0 && oi == 0) {
@@ -267,101 +271,112 @@ size_t cross_root_lds_bytes(int np, int d) {
 
 // ---------------------------------------------------------------------------
 // posterior_cov_kernel: cov[b][k] = s k(x_b, D_k) - sum_l Q[b][l] Q_D[k][l]
-// One workgroup per 16x16 output tile (ti candidates x tk points) per output;
-// the 4 waves split the n_pad/4 k-blocks; each wave issues the loads of a
-// whole batch of PC_U k-blocks (2 x 512-byte coalesced fragment loads per
-// k-block) before its MFMAs, so the L2 latency is paid once per batch.
-// Partials are reduced in LDS in fixed wave order.
-constexpr int PC_WAVES = 4;
-constexpr int PC_U = 16;
+// One workgroup (8 waves) per 32 x 32 block = 2 x 2 output tiles of one
+// output; wave w computes tile (w & 3) over K-half (w >> 2).  The two waves
+// of a tile that share a K-half of an operand tile read it at the same time,
+// so a CU fetches each operand byte about once (L1); every load is a 16-byte
+// pair (two k-blocks).  K-halves meet in LDS; the K-half-0 wave evaluates
+// the kernel epilogue and stores.  Tiles with tk == 0 also produce the
+// candidates' own variances s - |Q_X[b]|^2.
+constexpr int PC_WAVES = 8;
+constexpr int PC_P = 8;  // 16-byte pairs per operand per load batch (16 k-blocks)
 
-// 4 workgroups per CU (<= 128 VGPRs): the whole 1024-workgroup headline grid is resident at once.
 template <int DM>
-__global__ __launch_bounds__(PC_WAVES * WAVE, 4) void posterior_cov_kernel(const Plan* __restrict__ P,
-                                                                         const double* __restrict__ xnew, int B) {
-  __shared__ __attribute__((aligned(16))) double part[PC_WAVES * 4 * 64];
-  __shared__ double qpart[PC_WAVES * 16];
-  unsigned long long* st = kst_slot(P->debug_stamp, 1);
+__global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
+                                                                         const double* __restrict__ xnew, int B,
+                                                                         int dst) {
+  __shared__ __attribute__((aligned(16))) double part[4 * 4 * 64];  // K-half 1 partial tiles
+  __shared__ double qpart[4 * 16];
+  unsigned long long* st = kst_slot(dst, 1);
   KST_BEGIN(st);
-  const int tk = blockIdx.x;
-  const int ti = blockIdx.y;
   const int oi = blockIdx.z;
   const dkg_output& o = P->o[oi];
   const int N = P->N;
   const int dbg = P->debug_cov;
-  if (tk > 0 && tk * 16 >= N) return;  // tile 0 always runs: it also produces the candidates' variances
-  const bool have_d = N > 0;
-  const int KB = pad16(o.n) / 4;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tt = wave & 3, half = wave >> 2;
+  const int ti = 2 * blockIdx.y + (tt >> 1);
+  const int tk = 2 * blockIdx.x + (tt & 1);
+  const int KB = pad16(o.n) / 4;
+  const bool have_d = N > 0;
+  // tiles that exist in the workspace / state buffers (wave-uniform)
+  const bool live = ti * 16 < pad16(B) && (tk * 16 < pad16(N) || (tk == 0 && !have_d));
+  const bool want_var = tk == 0;
+  // K-half of this wave, in whole 16-byte pairs
+  const int KP = KB / 2;
+  const int p0 = half * ((KP + 1) / 2), p1 = half ? KP : (KP + 1) / 2;
 
-  const int chunk = (KB + PC_WAVES - 1) / PC_WAVES;
-  const int k0 = wave * chunk;
-  const int k1 = min(KB, k0 + chunk);
-  const double* qa = P->q[oi] + (size_t)ti * KB * 64 + lane;
-  const double* qd = o.disc_frag + (size_t)tk * KB * 64 + lane;
-  // four independent accumulation chains (k-block mod 4): the f64 MFMA
-  // dependent-issue latency is hidden by the other chains
-  // epilogue operands (row b, column k of register r = wave) first: their
-  // latency overlaps the fragment loads
-  const int b = ti * 16 + (lane >> 4) + 4 * wave;
-  const int k = tk * 16 + (lane & 15);
+  // epilogue operands first (row b = 16 ti + (l >> 4) + 4 r, column k = 16 tk + (l & 15))
   const int d = P->d;
-  const double* xb = xnew + (size_t)min(b, B - 1) * d;
-  const double* xk = have_d ? P->disc + (size_t)min(k, N - 1) * d : xb;
-  const double r2 = scaled_r2_dm<DM>(xb, xk, o.inv_lengthscale, d);
+  const int k = tk * 16 + (lane & 15);
+  double r2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (half == 0) {  // wave-uniform; P->disc is valid even when N == 0 (plan init)
+    const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = ti * 16 + (lane >> 4) + 4 * r;
+      r2[r] = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d);
+    }
+  }
   KST(st, 2);
   d4 acc[4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-  double qsq = 0.0;  // lane l: sum over this wave's k of Q_X[16 ti + (l & 15)][k]^2 (k = 4 kb + (l >> 4))
-  for (int base = k0; base < k1; base += PC_U) {
-    double ra[PC_U], rb[PC_U];
+  double qsq = 0.0;  // lane l: sum over this wave's k of Q_X[16 ti + (l & 15)][k]^2
+  if (live) {
+    for (int pb = p0; pb < p1; pb += PC_P) {
+      double2 va[PC_P], vd[PC_P];
+      // disc_frag tile 0 exists only when N > 0: the N == 0 variance-only
+      // wave reads its own Q_X tile as a stand-in (multiplied by 0 below)
+      const double* dsrc = have_d ? o.disc_frag : P->q[oi];
+      const int dt = have_d ? tk : ti;
 #pragma unroll
-    for (int u = 0; u < PC_U; ++u) {
-      const int kb = min(base + u, KB - 1);
-      if (dbg & 1) {
-        ra[u] = 1.0 + kb;
-        rb[u] = 0.5;
-      } else {
-        ra[u] = qa[(size_t)kb * 64];
-        rb[u] = (have_d && base + u < k1) ? qd[(size_t)kb * 64] : 0.0;
+      for (int u = 0; u < PC_P; ++u) {
+        const int j = min(pb + u, p1 - 1);
+        va[u] = frag_pair(P->q[oi], ti, j, lane, KB);
+        vd[u] = frag_pair(dsrc, dt, j, lane, KB);
       }
-    }
-    if (dbg & 2) {
+      if (dbg & 1) {
 #pragma unroll
-      for (int u = 0; u < PC_U; ++u) acc[0][u & 3] += ra[u] * rb[u];
-      continue;
-    }
+        for (int u = 0; u < PC_P; ++u) { va[u] = double2{1.0, 1.0}; vd[u] = double2{0.5, 0.5}; }
+      }
 #pragma unroll
-    for (int u = 0; u < PC_U; ++u) acc[u & 3] = mfma_f64(ra[u], rb[u], acc[u & 3]);
-    if (tk == 0) {  // the candidates' own |Q_X[b]|^2 (padding k-blocks of the batch repeat the last one)
-#pragma unroll
-      for (int u = 0; u < PC_U; ++u) qsq = (base + u < k1) ? fma(ra[u], ra[u], qsq) : qsq;
+      for (int u = 0; u < PC_P; ++u) {
+        const bool in = pb + u < p1 && have_d;
+        const double a0 = va[u].x, a1 = va[u].y;
+        const double d0 = in ? vd[u].x : 0.0, d1 = in ? vd[u].y : 0.0;
+        acc[(2 * u) & 3] = mfma_f64(a0, d0, acc[(2 * u) & 3]);
+        acc[(2 * u + 1) & 3] = mfma_f64(a1, d1, acc[(2 * u + 1) & 3]);
+        if (want_var) qsq = (pb + u < p1) ? fma(a1, a1, fma(a0, a0, qsq)) : qsq;
+      }
     }
   }
   const d4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   KST(st, 3);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) part[(wave * 4 + r) * 64 + lane] = accs[r];
-  if (tk == 0) {
+  if (want_var) {
     qsq += __shfl_xor(qsq, 16);
     qsq += __shfl_xor(qsq, 32);
-    if (lane < 16) qpart[wave * 16 + lane] = qsq;
+  }
+  if (half == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[(tt * 4 + r) * 64 + lane] = accs[r];
+    if (want_var && lane < 16) qpart[tt * 16 + lane] = qsq;
   }
   __syncthreads();
-  if (tk == 0 && threadIdx.x < 16) {
-    const int bb = ti * 16 + threadIdx.x;
-    double q2 = 0.0;
-#pragma unroll
-    for (int w = 0; w < PC_WAVES; ++w) q2 += qpart[w * 16 + threadIdx.x];
-    if (bb < B) P->var[oi][bb] = o.outputscale - q2;
-  }
-
   KST(st, 4);
-  double s = 0.0;
+  if (half == 0 && live) {
 #pragma unroll
-  for (int w = 0; w < PC_WAVES; ++w) s += part[(w * 4 + wave) * 64 + lane];
-  if (b < B && k < N)
-    P->cov[oi][(size_t)b * N + k] = ((dbg & 4) ? r2 : o.outputscale * kernel_profile(o.kernel, r2)) - s;
+    for (int r = 0; r < 4; ++r) {
+      const double sum = accs[r] + part[(tt * 4 + r) * 64 + lane];
+      const int b = ti * 16 + (lane >> 4) + 4 * r;
+      if (b < B && k < N)
+        P->cov[oi][(size_t)b * N + k] =
+            ((dbg & 4) ? r2[r] : o.outputscale * kernel_profile(o.kernel, r2[r])) - sum;
+    }
+    if (want_var && lane < 16) {
+      const int bb = ti * 16 + lane;
+      if (bb < B) P->var[oi][bb] = o.outputscale - (qsq + qpart[tt * 16 + lane]);
+    }
+  }
   KST_END(st);
 }
 
@@ -431,13 +446,23 @@ __device__ __forceinline__ double envelope_walk(const double (&la)[MAXL], const 
   return kg;
 }
 
-// KG of one set of lines held MAXL per lane (line k in lane k % 64, slot k / 64).
+// Result of the register passes over one set of lines.
+struct EnvFilter {
+  double bL, aL, bR, aR, bT, aT;
+  int cnt;      // survivors written to the LDS list (the list then holds L, T, R at cnt..cnt+2)
+  int status;   // 0: list ready, 1: KG = 0 (short-circuit), 2: list overflow (caller walks the lines)
+};
+
+// Register passes over one set of lines held MAXL per lane (line k in lane
+// k % 64, slot k / 64): extremes, exact ties, and the survivors of the chord
+// filter compacted into the wave's LDS list (sb, sa).
 template <int MAXL>
-__device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
-                                              double* sb, double* sa, int* nhull) {
-  // ---- extremes by value, then exact tie passes (exec-masked, rarely taken):
+__device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], const double (&lb)[MAXL], int lane,
+                                                     double* sb, double* sa) {
+  EnvFilter f;
+  // ---- extremes by value, then exact tie passes:
   // L = min b (tie: max a), R = max b (tie: max a), T = max a (tie: min b).
-  // (slots beyond nl hold padding lines: a = -inf, b = a real slope)
+  // (slots beyond the line count hold padding lines: a = -inf, b = a real slope)
   double bmin = INFINITY, bmax = -INFINITY, amax = -INFINITY;
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
@@ -453,8 +478,8 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
   // short-circuit of discretekg.py:363-367 (all |b| < 1e-9), and the
   // single-slope case (one hull vertex, E = max a): KG = 0.
   if (!uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax)) {
-    if (nhull) *nhull = 1;
-    return 0.0;
+    f.status = 1;
+    return f;
   }
   double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
 #pragma unroll
@@ -469,6 +494,7 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
     bT = fmin(bT, partner_f64<S_>(bT));
   })
   const double bL = bmin, bR = bmax, aT = amax;
+  f.bL = bL; f.aL = aL; f.bR = bR; f.aR = aR; f.bT = bT; f.aT = aT;
 
   // ---- survivors: lines strictly above the chord L-T or the chord T-R.
   // No left/right select is needed: every line has a <= aT, so a line left of
@@ -476,7 +502,7 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
   // of T never above the extension of L-T (slope >= 0); a degenerate chord
   // (db = 0) admits nothing.  h = (a - a0) db - (b - b0) da > 0, evaluated as
   // a*db - b*da > a0*db - b0*da.  Rounding can only admit extra lines (L, T
-  // or R themselves), which the exact test below discards.
+  // or R themselves), which the exact test in envelope_hull discards.
   const double db1 = bT - bL, da1 = aT - aL, k1 = aL * db1 - bL * da1;
   const double db2 = bR - bT, da2 = aR - aT, k2 = aT * db2 - bT * da2;
   int cnt = 0;
@@ -493,46 +519,66 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
       cnt += __popcll(mk);
     }
   }
-  if (cnt + 3 > ENV_CAP) return envelope_walk<MAXL>(la, lb, nl, lane, bL, aL, bR, bT, nhull);
+  f.cnt = cnt;
+  f.status = (cnt + 3 > ENV_CAP) ? 2 : 0;
+  return f;
+}
+
+// Exact upper envelope of the candidate list (survivors + L, T, R) and the
+// cancellation-free expectation; needs no register lines.
+__device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, double* sb, double* sa, int* nhull,
+                                                int dbg = 0) {
+  const int cnt = f.cnt;
+  const double bT = f.bT;
   if (lane == 0) {
-    sb[cnt] = bL; sa[cnt] = aL;
-    sb[cnt + 1] = bT; sa[cnt + 1] = aT;
-    sb[cnt + 2] = bR; sa[cnt + 2] = aR;
+    sb[cnt] = f.bL; sa[cnt] = f.aL;
+    sb[cnt + 1] = f.bT; sa[cnt + 1] = f.aT;
+    sb[cnt + 2] = f.bR; sa[cnt + 2] = f.aR;
   }
   const int nc = cnt + 3;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
+  if (dbg & 1024) return sb[lane & 7];  // ablation: list only
   // ---- right neighbour of every candidate P (one per lane, two chunks of 64
   // at most): the line that takes over from P as z grows, i.e. the reference
   // walk's step (discretekg.py:382-401): argmin over b_Q > b_P of the
   // intersection (a_P - a_Q)/(b_Q - b_P), ties -> larger slope.  Compared by
-  // cross multiplication (both denominators > 0).
+  // cross multiplication (both denominators > 0).  The list is read from LDS
+  // once; candidate Q = j is broadcast from lane j's register (v_readlane),
+  // and the selection is branch-free.
+  double lb_[2], la_[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int e = min(c * 64 + lane, nc - 1);
+    lb_[c] = sb[e];
+    la_[c] = sa[e];
+  }
   int nxt[2] = {-1, -1};
   double cn[2] = {0.0, 0.0}, cd[2] = {1.0, 1.0}, cb[2] = {0.0, 0.0}, pb[2] = {0.0, 0.0};
+  const int nc0 = min(nc, 64);
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     if (c * 64 >= nc) break;
-    const int e = c * 64 + lane;
-    const bool mine = e < nc;
-    const double bP = mine ? sb[e] : 0.0, aP = mine ? sa[e] : 0.0;
+    const double bP = lb_[c], aP = la_[c];
     double rn = 0.0, rd = 1.0, rb = 0.0;
     int rj = -1;
-#pragma unroll 4
-    for (int j = 0; j < nc; ++j) {
-      const double bQ = sb[j], aQ = sa[j];
+    auto consider = [&](double bQ, double aQ, int j) {
       const double num = aP - aQ, den = bQ - bP;
       const double x = num * rd, y = rn * den;
-      const bool take = den > 0.0 && (rj < 0 || x < y || (x == y && bQ > rb));
+      const bool take = (den > 0.0) & ((rj < 0) | (x < y) | ((x == y) & (bQ > rb)));
       rn = take ? num : rn;
       rd = take ? den : rd;
       rb = take ? bQ : rb;
       rj = take ? j : rj;
-    }
+    };
+#pragma unroll 4
+    for (int j = 0; j < nc0; ++j) consider(readlane_f64(lb_[0], j), readlane_f64(la_[0], j), j);
+    for (int j = 64; j < nc; ++j) consider(readlane_f64(lb_[1], j - 64), readlane_f64(la_[1], j - 64), j);
     nxt[c] = rj; cn[c] = rn; cd[c] = rd; cb[c] = rb; pb[c] = bP;
   }
 
+  if (dbg & 2048) return cn[0] + cd[1] + (double)nxt[0];  // ablation: + right neighbours
   // ---- follow the chain from L (index cnt): its members are the envelope
   // lines in increasing slope, ending at R (no right neighbour).
   uint64_t on0 = 0, on1 = 0;
@@ -542,6 +588,7 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
     ++h;
     cur = (cur < 64) ? __builtin_amdgcn_readlane(nxt[0], cur) : __builtin_amdgcn_readlane(nxt[1], cur - 64);
   }
+  if (dbg & 4096) return (double)(on0 + on1) + cn[0];  // ablation: + chain walk
   // ---- each envelope line other than R contributes its right edge P -> Q:
   //   (b_Q - b_P) psi(+-c), minus sign when the edge ends at or left of T.
   double v = 0.0;
@@ -551,11 +598,26 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
     const bool on = (((c == 0) ? on0 : on1) >> lane) & 1;
     if (on && nxt[c] >= 0) {
       const double cc = cn[c] / cd[c];
-      v += (cb[c] - pb[c]) * psi((cb[c] <= bT) ? -cc : cc);
+      const double sc = (cb[c] <= bT) ? -cc : cc;
+      v += (cb[c] - pb[c]) * ((dbg & 64) ? sc * sc : psi(sc));  // 64: ablation, psi -> c^2
     }
   }
   if (nhull) *nhull = h;
   return wave_sum(v);
+}
+
+
+// Whole envelope stage for register-held lines (lines_kg_kernel).
+template <int MAXL>
+__device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
+                                              double* sb, double* sa, int* nhull) {
+  const EnvFilter f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
+  if (f.status == 1) {
+    if (nhull) *nhull = 1;
+    return 0.0;
+  }
+  if (f.status == 2) return envelope_walk<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bR, f.bT, nhull);
+  return envelope_hull(f, lane, sb, sa, nhull);
 }
 
 // Debug phase stamps (debug_flags & 4): [wave][8] s_memtime values.
@@ -589,7 +651,7 @@ __device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, doubl
 
 template <int MAXL, int M>
 __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
-                                                       double* __restrict__ pairs_out) {
+                                                       double* __restrict__ pairs_out, int dst) {
   __shared__ double s_tail[16];
   __shared__ double s_sv[DKG_MAX_OUTPUTS];   // noiseless posterior variance at x_b, per output
   __shared__ double s_mx[DKG_MAX_OUTPUTS];   // posterior mean at x_b (model space), per output
@@ -608,7 +670,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   const bool full = target < 0;
   const int SL = stage_len(N);
   DKG_STAMP(0);
-  unsigned long long* st = kst_slot(P->debug_stamp, 2);
+  unsigned long long* st = kst_slot(dst, 2);
   KST_BEGIN(st);
 
   // Per-output scalars, hoisted once (static kernarg offsets).
@@ -685,75 +747,93 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     }
     // ---- lines: slot t of lane l is line k = l + 64 t (k = 0: the candidate).
     // Branch-free bodies (one LDS read stream per array, no per-slot waits):
-    // unused output slots read output 0 with a zero weight.
-    const double* mup[M];
+    // unused output slots read output 0 with a zero weight.  Rebuilt from the
+    // staged LDS data when the survivor list overflows, so the register copy
+    // is dead once the filter has run.
+    auto build_lines = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
+      const double* mup[M];
 #pragma unroll
-    for (int i = 0; i < M; ++i) mup[i] = lmu + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
-    double la[MAXL], lb[MAXL];
-    if (dbg & 16) {  // ablation: no line build (synthetic lines)
+      for (int i = 0; i < M; ++i) mup[i] = lmu + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
+      if (full) {
+        const double* cvp[M];
 #pragma unroll
-      for (int t = 0; t < MAXL; ++t) {
-        la[t] = a_off * (double)(lane + t);
-        lb[t] = wb[0] * (double)(lane - t);
+        for (int i = 0; i < M; ++i) cvp[i] = lcv + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
+#pragma unroll
+        for (int t = 0; t < MAXL; ++t) {
+          double a = a_off, bb = 0.0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            a = fma(wa[i], mup[i][64 * t], a);
+            bb = fma(wb[i], cvp[i][64 * t], bb);
+          }
+          la[t] = a;
+          lb[t] = bb;
+        }
+      } else {
+        const double* cvt = lcv + (size_t)target * SLp + lane - 1;
+        double wbt = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
+#pragma unroll
+        for (int t = 0; t < MAXL; ++t) {
+          double a = a_off;
+#pragma unroll
+          for (int i = 0; i < M; ++i) a = fma(wa[i], mup[i][64 * t], a);
+          la[t] = a;
+          lb[t] = wbt * cvt[64 * t];
+        }
       }
-    } else if (full) {
-      const double* cvp[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) cvp[i] = lcv + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
-#pragma unroll
-      for (int t = 0; t < MAXL; ++t) {
-        double a = a_off, bb = 0.0;
+      {
+        double a = a_off, bb = 0.0;  // line 0: the candidate itself (discretekg.py:182-183)
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          a = fma(wa[i], mup[i][64 * t], a);
-          bb = fma(wb[i], cvp[i][64 * t], bb);
+          a = fma(wa[i], mx0[i], a);
+          bb = fma(wb[i], sv[i], bb);
         }
-        la[t] = a;
-        lb[t] = bb;
+        la[0] = (lane == 0) ? a : la[0];
+        lb[0] = (lane == 0) ? bb : lb[0];
       }
-    } else {
-      const double* cvt = lcv + (size_t)target * SLp + lane - 1;
-      double wbt = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
-#pragma unroll
-      for (int t = 0; t < MAXL; ++t) {
-        double a = a_off;
-#pragma unroll
-        for (int i = 0; i < M; ++i) a = fma(wa[i], mup[i][64 * t], a);
-        la[t] = a;
-        lb[t] = wbt * cvt[64 * t];
-      }
-    }
-    {
-      double a = a_off, bb = 0.0;  // line 0: the candidate itself (discretekg.py:182-183)
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        a = fma(wa[i], mx0[i], a);
-        bb = fma(wb[i], sv[i], bb);
-      }
-      la[0] = (lane == 0) ? a : la[0];
-      lb[0] = (lane == 0) ? bb : lb[0];
-    }
-    {  // padding lines beyond N: never maximal, never change min/max slope
+      // padding lines beyond N (only in the last slots): never maximal, never
+      // change the min/max slope
       const double bfill = __shfl(lb[0], 0);
 #pragma unroll
       for (int t = 0; t < MAXL; ++t) {
-        const bool pad = lane + 64 * t > N;
-        la[t] = pad ? -INFINITY : la[t];
-        lb[t] = pad ? bfill : lb[t];
+        if (64 * t + 63 > N) {  // wave-uniform
+          const bool pad = lane + 64 * t > N;
+          la[t] = pad ? -INFINITY : la[t];
+          lb[t] = pad ? bfill : lb[t];
+        }
       }
-    }
-    DKG_STAMP(2);
+    };
 
     double kgj;
-    if (dbg & 1) {  // ablation: lines + one reduction only
-      double mxv = -INFINITY;
+    EnvFilter f;
+    {
+      double la[MAXL], lb[MAXL];
+      build_lines(la, lb);
+      DKG_STAMP(2);
+      if (dbg & 1) {  // ablation: lines + one reduction only
+        double mxv = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < MAXL; ++t) mxv = fmax(mxv, la[t] + lb[t]);
-      kgj = wave_max(mxv);
-    } else {
-      kgj = envelope_kg<MAXL>(la, lb, NL, lane, sb, sa, nullptr);
+        for (int t = 0; t < MAXL; ++t) mxv = fmax(mxv, la[t] + lb[t]);
+        f.status = 3;
+        f.aT = wave_max(mxv);
+      } else {
+        f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
+      }
+    }
+    if (f.status == 3) {
+      kgj = f.aT;
+    } else if (f.status == 1) {
+      kgj = 0.0;
+    } else if (dbg & 32) {  // debug: report the candidate count instead of KG
+      kgj = (double)(f.cnt + 3);
+    } else if (f.status == 0) {
+      kgj = envelope_hull(f, lane, sb, sa, nullptr, dbg);
+    } else {  // list overflow: gift wrap over the (rebuilt) register lines
+      double la[MAXL], lb[MAXL];
+      build_lines(la, lb);
+      kgj = envelope_walk<MAXL>(la, lb, NL, lane, f.bL, f.aL, f.bR, f.bT, nullptr);
     }
     DKG_STAMP(3);
     if (pairs_out != nullptr && lane == 0) pairs_out[(size_t)b * S + j] = kgj;
@@ -902,11 +982,12 @@ static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const doubl
     if (lds > 65536)
       (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds);
-    hipLaunchKernelGGL(cross_root_plan_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg);
+    hipLaunchKernelGGL(cross_root_plan_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
+                       h.debug_stamp);
     return hipGetLastError();
   }
-  dim3 grid(std::max(1, pad16(h.N) / 16), pad16(B) / 16, h.m);
-  hipLaunchKernelGGL(posterior_cov_kernel<DM>, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B);
+  dim3 grid(std::max(1, (h.N + 31) / 32), (B + 31) / 32, h.m);
+  hipLaunchKernelGGL(posterior_cov_kernel<DM>, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B, h.debug_stamp);
   return hipGetLastError();
 }
 
@@ -922,22 +1003,22 @@ void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {
 
 template <int MAXL, int M>
 static hipError_t launch_env_t(const Plan* dev, int B, double* kg, double* pairs, dim3 grid, dim3 block, size_t lds,
-                               hipStream_t s) {
+                               hipStream_t s, int dst) {
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-  hipLaunchKernelGGL((envelope_kernel<MAXL, M>), grid, block, lds, s, dev, B, kg, pairs);
+  hipLaunchKernelGGL((envelope_kernel<MAXL, M>), grid, block, lds, s, dev, B, kg, pairs, dst);
   return hipGetLastError();
 }
 
 template <int M>
 static hipError_t launch_env_m(int lines, const Plan* dev, int B, double* kg, double* pairs, dim3 grid, dim3 block,
-                               size_t lds, hipStream_t s) {
-  if (lines <= 64 * 2) return launch_env_t<2, M>(dev, B, kg, pairs, grid, block, lds, s);
-  if (lines <= 64 * 4) return launch_env_t<4, M>(dev, B, kg, pairs, grid, block, lds, s);
-  if (lines <= 64 * 8) return launch_env_t<8, M>(dev, B, kg, pairs, grid, block, lds, s);
-  if (lines <= 64 * 17) return launch_env_t<17, M>(dev, B, kg, pairs, grid, block, lds, s);
-  if (lines <= 64 * 33) return launch_env_t<33, M>(dev, B, kg, pairs, grid, block, lds, s);
+                               size_t lds, hipStream_t s, int dst) {
+  if (lines <= 64 * 2) return launch_env_t<2, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
+  if (lines <= 64 * 4) return launch_env_t<4, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
+  if (lines <= 64 * 8) return launch_env_t<8, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
+  if (lines <= 64 * 17) return launch_env_t<17, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
+  if (lines <= 64 * 33) return launch_env_t<33, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
   return hipErrorInvalidValue;
 }
 
@@ -956,11 +1037,11 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
   dim3 grid(B, h.split), block(h.sw * WAVE);
   const size_t lds = envelope_lds_bytes(h.m, h.N, h.sw, h.S);
   switch (outputs_bucket(h.m)) {
-    case 1: return launch_env_m<1>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
-    case 2: return launch_env_m<2>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
-    case 3: return launch_env_m<3>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
-    case 4: return launch_env_m<4>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
-    default: return launch_env_m<8>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s);
+    case 1: return launch_env_m<1>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
+    case 2: return launch_env_m<2>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
+    case 3: return launch_env_m<3>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
+    case 4: return launch_env_m<4>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
+    default: return launch_env_m<8>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
   }
 }
 

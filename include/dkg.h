@@ -21,11 +21,13 @@
  *
  * Data layout in HBM (see DESIGN.md "Data layout"):
  *   n_pad(n) = n rounded up to a multiple of 16.
- *   A "fragment-packed" matrix P (rows x n, rows padded to 16) is stored as
- *   F[t][kb][l] = P[16 t + (l & 15)][4 kb + (l >> 4)],  t < rows_pad/16,
- *   kb < n_pad/4, l < 64 — exactly the per-lane operand order of
- *   v_mfma_f64_16x16x4_f64, so every MFMA operand load is one coalesced
- *   512-byte read.  Padding entries are zero.
+ *   A "fragment-packed" matrix P (rows x n, rows padded to 16, KB = n_pad/4
+ *   k-blocks) is stored pair-packed:
+ *     F[t][j][l][h] = P[16 t + (l & 15)][4 (2 j + h) + (l >> 4)],
+ *   t < rows_pad/16, j < KB/2, l < 64, h < 2 — the per-lane operand order of
+ *   v_mfma_f64_16x16x4_f64 for k-blocks 2j and 2j+1 side by side, so one
+ *   coalesced 16-byte-per-lane (1 KiB) load feeds two MFMAs.  Padding entries
+ *   are zero.
  */
 #ifndef DKG_AMD_DKG_H
 #define DKG_AMD_DKG_H
@@ -67,7 +69,7 @@ typedef struct dkg_output {
   const double* inv_lengthscale; /* device [d]: 1 / ARD lengthscale */
   const double* train_x;     /* device [n x d] row-major (normalised inputs) */
   const double* alpha;       /* device [n_pad(n)], zero padded */
-  const double* root_frag;   /* device, fragment-packed R^T view: F[tj][kb][l] = R[4kb+(l>>4)][16tj+(l&15)], n_pad^2 */
+  const double* root_frag;   /* device, fragment-packed R^T (P[c][r] = R[r][c]), n_pad^2 */
   const double* disc_frag;   /* device, fragment-packed Q_D = K(D,X) R: N_pad x n_pad (nullable for dkg_cross_root) */
   const double* disc_mean;   /* device [N]: c + K(D,X) alpha, model space (nullable for dkg_cross_root) */
 } dkg_output;

@@ -141,8 +141,9 @@ def test_cross_root_matches_dense_product():
         N = D.shape[0]
         npad = (n + 15) // 16 * 16
         Npad = (N + 15) // 16 * 16
-        F = c.disc_frag.cpu().reshape(Npad // 16, npad // 4, 4, 16)  # [t][kb][l>>4][l&15]
-        dense = F.permute(0, 3, 1, 2).reshape(Npad, npad)[:N, :n]
+        # pair-packed: [t][j][l>>4][l&15][h] = P[16t + (l&15)][4(2j+h) + (l>>4)]
+        F = c.disc_frag.cpu().reshape(Npad // 16, npad // 8, 4, 16, 2)
+        dense = F.permute(0, 3, 1, 4, 2).reshape(Npad, npad)[:N, :n]
         torch.testing.assert_close(dense, Qd, rtol=1e-8, atol=1e-8)
 
 
