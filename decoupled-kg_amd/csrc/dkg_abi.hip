@@ -32,6 +32,8 @@ int hip_check(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct WsLayout {
+  size_t jq[DKG_MAX_OUTPUTS];
+  size_t gmu[DKG_MAX_OUTPUTS];
   size_t q[DKG_MAX_OUTPUTS];
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
@@ -41,11 +43,17 @@ struct WsLayout {
   size_t total;
 };
 
-WsLayout layout(const dkg_output* outs, int m, int N, int B, int S) {
+WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, int flags = 0) {
   WsLayout L{};
   size_t off = 0;
   const size_t Bp = pad16(std::max(B, 1));
   for (int i = 0; i < m; ++i) {
+    if (flags & DKG_PLAN_GRAD) {
+      L.jq[i] = off;
+      off = align256(off + (size_t)d * Bp * pad16(outs[i].n) * sizeof(double));
+      L.gmu[i] = off;
+      off = align256(off + (size_t)d * Bp * sizeof(double));
+    }
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
     L.mux[i] = off;
@@ -83,7 +91,7 @@ int check_outputs(const dkg_output* outs, int m, int d) {
 }
 
 int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
-               int target, int max_B, void* workspace, size_t workspace_bytes, Plan* P) {
+               int target, int max_B, void* workspace, size_t workspace_bytes, Plan* P, int flags = 0) {
   int st = check_outputs(outs, m, d);
   if (st) return st;
   if (max_B < 0 || N < 0) return fail(DKG_ERR_ARG, "negative size B=%d N=%d", max_B, N);
@@ -98,7 +106,10 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
-  const WsLayout L = layout(outs, m, N, max_B, S);
+  if (flags & ~DKG_PLAN_GRAD) return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
+  if ((flags & DKG_PLAN_GRAD) && envelope_grad_lds_bytes(m, N, sw, S, d, 16) > 160 * 1024)
+    return fail(DKG_ERR_UNSUPPORTED, "gradient: m=%d outputs, N=%d, d=%d exceed the envelope stage's LDS", m, N, d);
+  const WsLayout L = layout(outs, m, N, max_B, S, d, flags);
   if (workspace_bytes < L.total)
     return fail(DKG_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, L.total);
   char* ws = static_cast<char*>(workspace);
@@ -114,9 +125,15 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->split = split;
   P->disc = (N > 0) ? disc : reinterpret_cast<const double*>(ws);  // always a readable address
   P->weights = weights;
+  P->grad = (flags & DKG_PLAN_GRAD) ? 1 : 0;
+  P->bpad = pad16(std::max(max_B, 1));
   for (int i = 0; i < m; ++i) {
     P->o[i] = outs[i];
     P->max_np = std::max(P->max_np, pad16(outs[i].n));
+    if (P->grad) {
+      P->jq[i] = reinterpret_cast<double*>(ws + L.jq[i]);
+      P->gmu[i] = reinterpret_cast<double*>(ws + L.gmu[i]);
+    }
     P->q[i] = reinterpret_cast<double*>(ws + L.q[i]);
     P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
     P->var[i] = reinterpret_cast<double*>(ws + L.var[i]);
@@ -130,6 +147,9 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
   static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
   P->debug_stamp = dst ? std::atoi(dst) : 0;
+  if (P->grad && envelope_grad_lds_bytes(m, N, sw, S, d, P->max_np) > 160 * 1024)
+    return fail(DKG_ERR_UNSUPPORTED, "gradient: n=%d training points, d=%d exceed the envelope stage's LDS",
+                P->max_np, d);
   return DKG_OK;
 }
 
@@ -264,17 +284,17 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
   return hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr), "forward");
 }
 
-size_t dkg_plan_workspace(const dkg_output* outs, int m, int N, int max_B, int S) {
+size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags) {
   if (!outs || m < 1 || m > DKG_MAX_OUTPUTS) return 0;
-  return layout(outs, m, N, max_B, S).total;
+  return layout(outs, m, N, max_B, S, d, flags).total;
 }
 
 int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
-                  int target, int max_B, void* workspace, size_t workspace_bytes, void* host_plan, void* dev_plan,
-                  void* stream) {
+                  int target, int max_B, int flags, void* workspace, size_t workspace_bytes, void* host_plan,
+                  void* dev_plan, void* stream) {
   if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
   Plan* h = static_cast<Plan*>(host_plan);
-  int st = build_plan(outs, m, d, disc, N, weights, S, target, max_B, workspace, workspace_bytes, h);
+  int st = build_plan(outs, m, d, disc, N, weights, S, target, max_B, workspace, workspace_bytes, h, flags);
   if (st) return st;
   return hip_check(hipMemcpyAsync(dev_plan, h, sizeof(Plan), hipMemcpyHostToDevice, (hipStream_t)stream),
                    "hipMemcpyAsync");
@@ -292,6 +312,19 @@ int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const do
   if (!host_plan || !dev_plan || !stage_ms) return fail(DKG_ERR_ARG, "NULL pointer");
   return run_forward(*static_cast<const Plan*>(host_plan), static_cast<const Plan*>(dev_plan), xnew, B, kg, kg_pairs,
                      (hipStream_t)stream, stage_ms);
+}
+
+int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                          double* dkg_dx, void* stream) {
+  if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  if (!h.grad) return fail(DKG_ERR_ARG, "plan was not initialised with DKG_PLAN_GRAD");
+  if (B < 0) return fail(DKG_ERR_ARG, "negative B=%d", B);
+  if (B == 0) return DKG_OK;
+  if (B > h.max_B) return fail(DKG_ERR_ARG, "B=%d candidates > plan capacity %d", B, h.max_B);
+  if (!xnew || !kg || !dkg_dx) return fail(DKG_ERR_ARG, "NULL data pointer");
+  return hip_check(launch_forward_grad(h, static_cast<const Plan*>(dev_plan), xnew, B, kg, dkg_dx,
+                                       (hipStream_t)stream), "forward_grad");
 }
 
 int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,

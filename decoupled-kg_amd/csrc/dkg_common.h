@@ -70,6 +70,38 @@ __device__ __forceinline__ double kernel_profile_t(double r2) {
   }
 }
 
+// h(r2) = kappa'(r) / r of the kernel profile, so that for the scaled
+// difference t = (x - z) / l:  d[s kappa(|t|)]/dx_j = s h(|t|^2) t_j / l_j.
+// Finite at r = 0 except Matern-1/2, whose gradient at a coincident point is
+// taken as 0 (GPyTorch clamps the distance there, which zeroes its gradient).
+template <int KIND>
+__device__ __forceinline__ double kernel_dprofile_t(double r2) {
+  if constexpr (KIND == DKG_RBF) {
+    return -exp(-0.5 * r2);
+  } else if constexpr (KIND == DKG_MATERN12) {
+    const double r = sqrt(r2);
+    return (r2 > 1e-30) ? -exp(-r) / r : 0.0;
+  } else if constexpr (KIND == DKG_MATERN32) {
+    return -3.0 * exp(-1.7320508075688772 * sqrt(r2));
+  } else {
+    const double t = 2.23606797749979 * sqrt(r2);
+    return -(5.0 / 3.0) * (1.0 + t) * exp(-t);
+  }
+}
+
+__device__ __forceinline__ double kernel_dprofile(int kind, double r2) {
+  switch (kind) {
+    case DKG_RBF: return kernel_dprofile_t<DKG_RBF>(r2);
+    case DKG_MATERN12: return kernel_dprofile_t<DKG_MATERN12>(r2);
+    case DKG_MATERN32: return kernel_dprofile_t<DKG_MATERN32>(r2);
+    default: return kernel_dprofile_t<DKG_MATERN52>(r2);
+  }
+}
+
+// Standard normal pdf and cdf (cdf via erfc: accurate in both tails).
+__device__ __forceinline__ double norm_pdf(double c) { return 0.3989422804014327 * exp(-0.5 * c * c); }
+__device__ __forceinline__ double norm_cdf(double c) { return 0.5 * erfc(-0.7071067811865476 * c); }
+
 __device__ __forceinline__ double scaled_r2(const double* __restrict__ xa, const double* __restrict__ xb,
                                             const double* __restrict__ il, int d) {
   double acc = 0.0;

@@ -16,12 +16,16 @@ struct Plan {
   int32_t sw, split;                // envelope geometry: waves per workgroup, workgroups per candidate
   int32_t debug_env, debug_cov;     // ablation switches (0 in production)
   int32_t debug_stamp;              // 1: per-workgroup phase stamps into g_kstamps (0 in production)
+  int32_t grad;                     // workspace holds the gradient buffers (DKG_PLAN_GRAD)
+  int32_t bpad;                     // pad16(max_B): rows of the fragment-packed candidate buffers
   const double* disc;               // [N x d]
   const double* weights;            // [S x m]
   double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
   double* mux[DKG_MAX_OUTPUTS];     // posterior mean at the candidates per output (workspace)
   double* var[DKG_MAX_OUTPUTS];     // noiseless posterior variance s - |Q_X[b]|^2 per output (workspace)
   double* cov[DKG_MAX_OUTPUTS];     // [B x N] posterior covariance rows per output (workspace)
+  double* jq[DKG_MAX_OUTPUTS];      // GRAD: d fragment-packed dK(x,X)/dx_g R matrices (bpad x n_pad each)
+  double* gmu[DKG_MAX_OUTPUTS];     // GRAD: [d][bpad] model-space mean gradients
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
   int* tickets;                     // [B] arrival counters (split > 2 only)
 };
@@ -39,6 +43,10 @@ hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, in
                                 double diag_add, double* out, hipStream_t s);
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
+// Value and gradient: kg[B] and dkg[B x d] (d KG(x_b) / d x_b), plan built with DKG_PLAN_GRAD.
+hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
+                               hipStream_t s);
+size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np);
 // One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                         hipStream_t s, int stage);

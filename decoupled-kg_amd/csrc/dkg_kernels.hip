@@ -81,10 +81,12 @@ __device__ __forceinline__ unsigned long long* kst_slot(int debug, int kid) {
 constexpr int CR_WAVES = 8;
 constexpr int CR_U = 8;  // k-blocks per load batch
 
-template <int DM>
+// GRAD: the same contraction with the kernel replaced by its derivative in
+// the candidate's coordinate `gdim` (J = dK(x, X)/dx_g R, dmean = dK/dx_g alpha).
+template <int DM, bool GRAD = false>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
                                                 double* __restrict__ qout, double* __restrict__ mout, int ti, int p,
-                                                double* smem, unsigned long long* st = nullptr) {
+                                                double* smem, unsigned long long* st = nullptr, int gdim = 0) {
   const int n = o.n;
   const int np = pad16(n);
   const int T = np / 16;
@@ -142,6 +144,10 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   // ---- fill K(x_row, X_col), col < 4*kbB, in B-operand order (zero outside)
   double mpart = 0.0;
   const double os = o.outputscale;
+  const double ilg = GRAD ? o.inv_lengthscale[gdim] : 1.0;
+  double xg = 0.0;  // the candidate's pre-scaled coordinate gdim (GRAD)
+#pragma unroll
+  for (int k = 0; k < DM; ++k) xg = (k == gdim) ? xr[k] : xg;
   const int fill = kbB * 64;
   const int iters = (fill + CR_WAVES * WAVE - 1) / (CR_WAVES * WAVE);  // uniform trip count
   // one straight-line loop per covariance family (the switch stays outside)
@@ -158,7 +164,12 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
         const double t = xr[k] - xs[(size_t)cc * d + min(k, d - 1)];
         r2 = fma(t, (k < d) ? t : 0.0, r2);
       }
-      const double kv = os * kernel_profile_t<KIND>(r2);
+      double kv;
+      if constexpr (GRAD) {
+        kv = os * kernel_dprofile_t<KIND>(r2) * (xg - xs[(size_t)cc * d + gdim]) * ilg;
+      } else {
+        kv = os * kernel_profile_t<KIND>(r2);
+      }
       const double v = (rv && col < n) ? kv : 0.0;
       const double al = als[cc];  // staged only when want_mean; otherwise ignored
       mpart = fma(v, want_mean ? al : 0.0, mpart);
@@ -235,7 +246,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
 #pragma unroll
     for (int w = 0; w < CR_WAVES; ++w) s += mred[w * 16 + tid];
     const int rr = ti * 16 + tid;
-    mout[rr] = (rr < rows) ? o.mean_constant + s : 0.0;
+    mout[rr] = (rr < rows) ? (GRAD ? s : o.mean_constant + s) : 0.0;
   }
   KST_END(st);
 }
@@ -263,6 +274,25 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
     }
   }
   cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
+}
+
+// Gradient cross stage: grid (B tiles, pairs, outputs x d); z = oi * d + g
+// writes J_g = dK(x, X)/dx_g R (fragment-packed) and dmean/dx_g for output oi.
+// Workgroup (0,0,0) clears the gradient accumulator dkg[B x d].
+template <int DM>
+__global__ __launch_bounds__(CR_WAVES * WAVE) void cross_grad_plan_kernel(const Plan* __restrict__ P,
+                                                                          const double* __restrict__ xnew, int B,
+                                                                          double* __restrict__ dkg, int dst) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  unsigned long long* st = kst_slot(dst, 0);
+  const int d = P->d;
+  const int oi = blockIdx.z / d, gdim = blockIdx.z % d;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+    for (int i = threadIdx.x; i < B * d; i += blockDim.x) dkg[i] = 0.0;
+  const dkg_output& o = P->o[oi];
+  const size_t mat = (size_t)P->bpad * pad16(o.n);
+  cross_root_impl<DM, true>(o, d, xnew, B, P->jq[oi] + gdim * mat, P->gmu[oi] + (size_t)gdim * P->bpad, blockIdx.x,
+                            blockIdx.y, smem, st, gdim);
 }
 
 size_t cross_root_lds_bytes(int np, int d) {
@@ -451,14 +481,29 @@ struct EnvFilter {
   double bL, aL, bR, aR, bT, aT;
   int cnt;      // survivors written to the LDS list (the list then holds L, T, R at cnt..cnt+2)
   int status;   // 0: list ready, 1: KG = 0 (short-circuit), 2: list overflow (caller walks the lines)
+  int kL, kT, kR;  // IDX: line indices of L, T, R (lowest index among exact duplicates)
+  int cntT;        // IDX: number of lines attaining max a (torch.max splits its gradient among them)
 };
+
+// Lowest line index k over the wave for which `hit` holds in the lane's slot (or a large value).
+template <int MAXL, class Pred>
+__device__ __forceinline__ int wave_first_index(int lane, Pred hit) {
+  int k = 1 << 30;
+#pragma unroll
+  for (int t = MAXL - 1; t >= 0; --t) k = hit(t) ? lane + 64 * t : k;
+  DKG_BUTTERFLY({
+    const int o = __shfl_xor(k, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
+    k = min(k, o);
+  })
+  return k;
+}
 
 // Register passes over one set of lines held MAXL per lane (line k in lane
 // k % 64, slot k / 64): extremes, exact ties, and the survivors of the chord
 // filter compacted into the wave's LDS list (sb, sa).
-template <int MAXL>
+template <int MAXL, bool IDX = false>
 __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], const double (&lb)[MAXL], int lane,
-                                                     double* sb, double* sa) {
+                                                     double* sb, double* sa, int* si = nullptr) {
   EnvFilter f;
   // ---- extremes by value, then exact tie passes:
   // L = min b (tie: max a), R = max b (tie: max a), T = max a (tie: min b).
@@ -514,13 +559,26 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
     if (mk != 0) {  // wave-uniform, rarely taken
       if (s) {
         const int pos = cnt + lanes_below(mk);
-        if (pos < ENV_CAP) { sb[pos] = bb; sa[pos] = a; }
+        if (pos < ENV_CAP) {
+          sb[pos] = bb;
+          sa[pos] = a;
+          if constexpr (IDX) si[pos] = lane + 64 * t;
+        }
       }
       cnt += __popcll(mk);
     }
   }
   f.cnt = cnt;
   f.status = (cnt + 3 > ENV_CAP) ? 2 : 0;
+  if constexpr (IDX) {
+    f.kL = wave_first_index<MAXL>(lane, [&](int t) { return lb[t] == bL && la[t] == aL; });
+    f.kT = wave_first_index<MAXL>(lane, [&](int t) { return la[t] == aT && lb[t] == bT; });
+    f.kR = wave_first_index<MAXL>(lane, [&](int t) { return lb[t] == bR && la[t] == aR; });
+    int c = 0;
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) c += __popcll(__ballot(la[t] == aT));
+    f.cntT = c;
+  }
   return f;
 }
 
@@ -607,6 +665,130 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
 }
 
 
+// ---------------------------------------------------------------------------
+// Vertex visitors for the gradient: the envelope lines in increasing slope,
+// each with its breakpoints (cL, cR) (-inf / +inf at the ends), passed to
+// visit(k, b, a, cL, cR); the return value is KG_w as in the forward.
+
+// From the candidate list of an IDX filter (si holds the line indices).
+template <class Visit>
+__device__ __forceinline__ double envelope_hull_visit(const EnvFilter& f, int lane, double* sb, double* sa, int* si,
+                                                      Visit&& visit) {
+  const int cnt = f.cnt;
+  const double bT = f.bT;
+  if (lane == 0) {
+    sb[cnt] = f.bL; sa[cnt] = f.aL; si[cnt] = f.kL;
+    sb[cnt + 1] = f.bT; sa[cnt + 1] = f.aT; si[cnt + 1] = f.kT;
+    sb[cnt + 2] = f.bR; sa[cnt + 2] = f.aR; si[cnt + 2] = f.kR;
+  }
+  const int nc = cnt + 3;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double lb_[2], la_[2];
+  int li_[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int e = min(c * 64 + lane, nc - 1);
+    lb_[c] = sb[e];
+    la_[c] = sa[e];
+    li_[c] = si[e];
+  }
+  int nxt[2] = {-1, -1};
+  double cn[2] = {0.0, 0.0}, cd[2] = {1.0, 1.0};
+  const int nc0 = min(nc, 64);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c * 64 >= nc) break;
+    const double bP = lb_[c], aP = la_[c];
+    double rn = 0.0, rd = 1.0, rb = 0.0;
+    int rj = -1;
+    auto consider = [&](double bQ, double aQ, int j) {
+      const double num = aP - aQ, den = bQ - bP;
+      const double x = num * rd, y = rn * den;
+      const bool take = (den > 0.0) & ((rj < 0) | (x < y) | ((x == y) & (bQ > rb)));
+      rn = take ? num : rn;
+      rd = take ? den : rd;
+      rb = take ? bQ : rb;
+      rj = take ? j : rj;
+    };
+#pragma unroll 4
+    for (int j = 0; j < nc0; ++j) consider(readlane_f64(lb_[0], j), readlane_f64(la_[0], j), j);
+    for (int j = 64; j < nc; ++j) consider(readlane_f64(lb_[1], j - 64), readlane_f64(la_[1], j - 64), j);
+    nxt[c] = rj; cn[c] = rn; cd[c] = rd;
+  }
+  // chain from L (index cnt) to R, one vertex per step
+  double kg = 0.0, cL = -INFINITY;
+  int cur = cnt;
+  for (int guard = 0; guard < nc; ++guard) {
+    const bool hi = cur >= 64;
+    const int ln = cur & 63;
+    const double bP = readlane_f64(hi ? lb_[1] : lb_[0], ln);
+    const double aP = readlane_f64(hi ? la_[1] : la_[0], ln);
+    const int kP = __builtin_amdgcn_readlane(hi ? li_[1] : li_[0], ln);
+    const int nx = __builtin_amdgcn_readlane(hi ? nxt[1] : nxt[0], ln);
+    double cR = INFINITY;
+    if (nx >= 0) {
+      cR = readlane_f64(hi ? cn[1] : cn[0], ln) / readlane_f64(hi ? cd[1] : cd[0], ln);
+      const double bQ = readlane_f64(nx >= 64 ? lb_[1] : lb_[0], nx & 63);
+      kg += (bQ - bP) * psi((bQ <= bT) ? -cR : cR);
+    }
+    visit(kP, bP, aP, cL, cR);
+    if (nx < 0) break;
+    cL = cR;
+    cur = nx;
+  }
+  return kg;
+}
+
+// Gift wrap over register lines with the line index carried (list overflow).
+template <int MAXL, class Visit>
+__device__ __forceinline__ double envelope_walk_visit(const double (&la)[MAXL], const double (&lb)[MAXL], int nl,
+                                                      int lane, const EnvFilter& f, Visit&& visit) {
+  double bc = f.bL, ac = f.aL, kg = 0.0, cL = -INFINITY;
+  int kc = f.kL;
+  for (int guard = 0; guard <= nl; ++guard) {
+    if (!uniform(bc < f.bR)) break;
+    double bn = INFINITY, bd = 1.0, bbest = -INFINITY, abest = -INFINITY;
+    int kbest = 1 << 30;
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const double bb = lb[t], a = la[t];
+      if (lane + 64 * t < nl && bb > bc) {
+        const double num = ac - a, den = bb - bc;
+        const double lhs = num * bd, rhs = bn * den;
+        if (bbest == -INFINITY || lhs < rhs || (lhs == rhs && (bb > bbest || (bb == bbest && a > abest)))) {
+          bn = num; bd = den; bbest = bb; abest = a; kbest = lane + 64 * t;
+        }
+      }
+    }
+    DKG_BUTTERFLY({
+      const double on = partner_f64<S_>(bn), od = partner_f64<S_>(bd);
+      const double ob = partner_f64<S_>(bbest), oa = partner_f64<S_>(abest);
+      const int ok = __shfl_xor(kbest, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
+      bool take;
+      if (ob == -INFINITY) take = false;
+      else if (bbest == -INFINITY) take = true;
+      else {
+        const double lhs = on * bd, rhs = bn * od;
+        take = lhs < rhs ||
+               (lhs == rhs && (ob > bbest || (ob == bbest && (oa > abest || (oa == abest && ok < kbest)))));
+      }
+      if (take) { bn = on; bd = od; bbest = ob; abest = oa; kbest = ok; }
+    })
+    if (!uniform(bbest > bc)) break;
+    const double c = bn / bd;
+    kg += (bbest - bc) * psi((bbest <= f.bT) ? -c : c);
+    visit(kc, bc, ac, cL, c);
+    cL = c;
+    bc = bbest;
+    ac = abest;
+    kc = __builtin_amdgcn_readfirstlane(kbest);
+  }
+  visit(kc, bc, ac, cL, INFINITY);
+  return kg;
+}
+
 // Whole envelope stage for register-held lines (lines_kg_kernel).
 template <int MAXL>
 __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
@@ -649,9 +831,12 @@ __device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, doubl
   }
 }
 
-template <int MAXL, int M>
+// GRAD: also dKG/dx_b (envelope theorem; include/dkg.h dkg_plan_forward_grad),
+// accumulated into dkg[b x d]; the extra LDS follows the survivor lists.
+template <int MAXL, int M, bool GRAD>
 __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
-                                                       double* __restrict__ pairs_out, int dst) {
+                                                       double* __restrict__ pairs_out, int dst,
+                                                       const double* __restrict__ xnew, double* __restrict__ dkg) {
   __shared__ double s_tail[16];
   __shared__ double s_sv[DKG_MAX_OUTPUTS];   // noiseless posterior variance at x_b, per output
   __shared__ double s_mx[DKG_MAX_OUTPUTS];   // posterior mean at x_b (model space), per output
@@ -691,6 +876,24 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   double* lcv = lmu + (size_t)M * SLp;
   double* lw = lcv + (size_t)M * SLp;
   double* sbuf = lw + ((S * m + 1) & ~1);
+  // GRAD regions: per-wave index lists, per-wave Q_D accumulators u_i[c], the
+  // candidate's q_i and J_i rows, gv / gm / per-wave gradient scratch, x_b.
+  const int d = P->d;
+  const int NP = P->max_np;
+  int* sidx = nullptr;
+  double *uacc = nullptr, *qrow = nullptr, *jrow = nullptr, *sgv = nullptr, *sgm = nullptr, *sgw = nullptr,
+         *sx = nullptr;
+  if constexpr (GRAD) {
+    double* gb = sbuf + (size_t)SW * 2 * ENV_CAP;
+    sidx = reinterpret_cast<int*>(gb);
+    uacc = gb + (SW * ENV_CAP + 1) / 2;
+    qrow = uacc + (size_t)SW * M * NP;
+    jrow = qrow + (size_t)M * NP;
+    sgv = jrow + (size_t)M * d * NP;                // [M][16]  d v_i / dx
+    sgm = sgv + M * DKG_MAX_DIM;                     // [M][16]  d mu_i / dx
+    sgw = sgm + M * DKG_MAX_DIM;                     // [SW][64] per wave: gacc | ga0 | gvv | gtot
+    sx = sgw + SW * 64;                              // [16]     x_b
+  }
 
   // ---- one round of memory traffic: DMA the line data, plain loads for the rest
 #pragma unroll
@@ -706,6 +909,26 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     s_sv[threadIdx.x] = P->var[threadIdx.x][b];
     s_mx[threadIdx.x] = P->mux[threadIdx.x][b];
   }
+  if constexpr (GRAD) {
+    // the candidate's q_i and J_i rows (fragment-packed in the workspace)
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i < m) {
+        const int npi = pad16(P->o[i].n), KBi = npi / 4;
+        const size_t mat = (size_t)P->bpad * npi;
+        for (int c = threadIdx.x; c < NP; c += blockDim.x) {
+          const size_t fi = frag_index(b >> 4, c >> 2, ((c & 3) << 4) | (b & 15), KBi);
+          qrow[(size_t)i * NP + c] = (c < npi) ? P->q[i][fi] : 0.0;
+          for (int dd = 0; dd < d; ++dd) jrow[((size_t)i * d + dd) * NP + c] = (c < npi) ? P->jq[i][dd * mat + fi] : 0.0;
+        }
+      }
+    }
+    if (threadIdx.x < m * d) {
+      const int i = threadIdx.x / d, dd = threadIdx.x % d;
+      sgm[i * DKG_MAX_DIM + dd] = P->gmu[i][(size_t)dd * P->bpad + b];
+    }
+    if (threadIdx.x < d) sx[threadIdx.x] = xnew[(size_t)b * d + threadIdx.x];
+  }
   KST(st, 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -715,6 +938,24 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
   double* sa = sb + ENV_CAP;
   double wave_acc = 0.0;
+  int* si = nullptr;
+  double *uw = nullptr, *gw = nullptr;
+  if constexpr (GRAD) {
+    si = sidx + (size_t)wave * ENV_CAP;
+    uw = uacc + (size_t)wave * M * NP;
+    gw = sgw + wave * 64;
+    // d v_i / dx = -2 J_i^T q_i (model space), one (output, coordinate) per wave
+    for (int pidx = wave; pidx < m * d; pidx += SW) {
+      const int i = pidx / d, dd = pidx % d;
+      double acc = 0.0;
+      for (int c = lane; c < NP; c += 64) acc = fma(jrow[((size_t)i * d + dd) * NP + c], qrow[(size_t)i * NP + c], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) sgv[i * DKG_MAX_DIM + dd] = -2.0 * acc;
+    }
+    for (int e = lane; e < M * NP; e += 64) uw[e] = 0.0;
+    for (int e = lane; e < 64; e += 64) gw[e] = 0.0;
+    __syncthreads();
+  }
   const int waves_total = SW * gridDim.y;
   double sv[M], mx0[M];
 #pragma unroll
@@ -808,7 +1049,105 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
 
     double kgj;
     EnvFilter f;
-    {
+    if constexpr (GRAD) {
+      {
+        double la[MAXL], lb[MAXL];
+        build_lines(la, lb);
+        f = envelope_filter<MAXL, true>(la, lb, lane, sb, sa, si);
+      }
+      double Vden = den;  // the variance under the square root of the slopes
+      if (!full) {
+        const double sd2 = ysd[target] * ysd[target];
+        Vden = sd2 * (sv[target] + nz[target]);
+      }
+      if (lane == 0) {
+        for (int dd = 0; dd < d; ++dd) {
+          double ga0 = 0.0, gvs = 0.0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            if (i < m) {
+              ga0 = fma(wa[i], sgm[i * DKG_MAX_DIM + dd], ga0);
+              const double cv = full ? w[i] * w[i] * ysd[i] * ysd[i] : ((i == target) ? ysd[i] * ysd[i] : 0.0);
+              gvs = fma(cv, sgv[i * DKG_MAX_DIM + dd], gvs);
+            }
+          }
+          gw[16 + dd] = ga0;
+          gw[32 + dd] = gvs / (2.0 * Vden);
+        }
+      }
+      double sumDb = 0.0;
+      // one envelope line: d/dx of its slope (and of line 0's intercept), weighted
+      // by dE/db = phi(cL) - phi(cR) and dE/da = Phi(cR) - Phi(cL)
+      auto visit = [&](int k, double bP, double aP, double cL, double cR) {
+        (void)aP;
+        const double Pw = norm_cdf(cR) - norm_cdf(cL);
+        const double Dw = norm_pdf(cL) - norm_pdf(cR);
+        sumDb = fma(Dw, bP, sumDb);
+        if (k == 0) {
+          if (lane == 0) {
+            for (int dd = 0; dd < d; ++dd) {
+              double gvs = 0.0;
+#pragma unroll
+              for (int i = 0; i < M; ++i)
+                if (i < m) gvs = fma(wb[i], sgv[i * DKG_MAX_DIM + dd], gvs);
+              gw[dd] += Dw * gvs + Pw * gw[16 + dd];
+            }
+          }
+        } else if (k <= N) {
+          const double* z = P->disc + (size_t)(k - 1) * d;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            if (i < m && wb[i] != 0.0) {
+              const dkg_output& o = P->o[i];
+              double r2 = 0.0;
+              for (int dd = 0; dd < d; ++dd) {
+                const double t = (sx[dd] - z[dd]) * o.inv_lengthscale[dd];
+                r2 = fma(t, t, r2);
+              }
+              const double coef = Dw * wb[i];
+              const double hc = coef * os[i] * kernel_dprofile(o.kernel, r2);
+              if (lane == 0)
+                for (int dd = 0; dd < d; ++dd) {
+                  const double il = o.inv_lengthscale[dd];
+                  gw[dd] += hc * (sx[dd] - z[dd]) * il * il;
+                }
+              const int npi = pad16(o.n), KBi = npi / 4, r = k - 1;
+              for (int c = lane; c < npi; c += 64)
+                uw[(size_t)i * NP + c] = fma(coef, o.disc_frag[frag_index(r >> 4, c >> 2, ((c & 3) << 4) | (r & 15), KBi)],
+                                             uw[(size_t)i * NP + c]);
+            }
+          }
+        }
+      };
+      if (f.status == 1) {
+        kgj = 0.0;
+      } else {
+        if (f.status == 0) {
+          kgj = envelope_hull_visit(f, lane, sb, sa, si, visit);
+        } else {
+          double la[MAXL], lb[MAXL];
+          build_lines(la, lb);
+          kgj = envelope_walk_visit<MAXL>(la, lb, NL, lane, f, visit);
+        }
+        // - sum_i J_i^T u_i, - sum_e Dw_e b_e * dV/(2V), - [line 0 attains max a] da_0/dx
+        for (int pidx = 0; pidx < m * d; ++pidx) {
+          const int i = pidx / d, dd = pidx % d;
+          double acc = 0.0;
+          for (int c = lane; c < NP; c += 64) acc = fma(jrow[((size_t)i * d + dd) * NP + c], uw[(size_t)i * NP + c], acc);
+          acc = wave_sum(acc);
+          if (lane == 0) gw[dd] -= acc;
+        }
+        double a0 = a_off;
+#pragma unroll
+        for (int i = 0; i < M; ++i) a0 = fma(wa[i], mx0[i], a0);
+        const double tfac = (a0 == f.aT) ? 1.0 / (double)f.cntT : 0.0;
+        if (lane == 0)
+          for (int dd = 0; dd < d; ++dd) gw[48 + dd] += gw[dd] - sumDb * gw[32 + dd] - tfac * gw[16 + dd];
+        for (int e = lane; e < M * NP; e += 64) uw[e] = 0.0;
+      }
+      if (lane == 0)
+        for (int dd = 0; dd < d; ++dd) gw[dd] = 0.0;
+    } else {
       double la[MAXL], lb[MAXL];
       build_lines(la, lb);
       DKG_STAMP(2);
@@ -822,7 +1161,8 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
         f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
       }
     }
-    if (f.status == 3) {
+    if constexpr (GRAD) {
+    } else if (f.status == 3) {
       kgj = f.aT;
     } else if (f.status == 1) {
       kgj = 0.0;
@@ -846,6 +1186,14 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   __syncthreads();
   DKG_STAMP(4);
   KST(st, 5);
+  if constexpr (GRAD) {
+    if (threadIdx.x < d) {
+      double gs = 0.0;
+      for (int w2 = 0; w2 < SW; ++w2) gs += sgw[w2 * 64 + 48 + threadIdx.x];
+      // at most two workgroups per candidate (S <= 16): commutative, deterministic
+      atomicAdd(&dkg[(size_t)b * d + threadIdx.x], gs / (double)S);
+    }
+  }
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int w2 = 0; w2 < SW; ++w2) s += s_tail[w2];
@@ -882,6 +1230,13 @@ size_t envelope_lds_bytes(int m, int N, int waves, int S) {
   const int M = outputs_bucket(m);
   return ((size_t)2 + 2 * (size_t)M * (stage_len(N) + 2) + ((S * m + 1) & ~1) + (size_t)waves * 2 * ENV_CAP) *
          sizeof(double);
+}
+
+size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np) {
+  const int M = outputs_bucket(m);
+  const size_t extra = (size_t)(waves * ENV_CAP + 1) / 2 + (size_t)waves * M * max_np + (size_t)M * max_np +
+                       (size_t)M * d * max_np + 2 * (size_t)M * DKG_MAX_DIM + (size_t)waves * 64 + DKG_MAX_DIM;
+  return envelope_lds_bytes(m, N, waves, S) + extra * sizeof(double);
 }
 
 // ---------------------------------------------------------------------------
@@ -1001,25 +1356,48 @@ void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {
   *split = (S + sw - 1) / sw;
 }
 
-template <int MAXL, int M>
-static hipError_t launch_env_t(const Plan* dev, int B, double* kg, double* pairs, dim3 grid, dim3 block, size_t lds,
-                               hipStream_t s, int dst) {
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL((envelope_kernel<MAXL, M>), grid, block, lds, s, dev, B, kg, pairs, dst);
+struct EnvLaunch {
+  const Plan* dev;
+  int B;
+  double* kg;
+  double* pairs;
+  dim3 grid, block;
+  size_t lds;
+  hipStream_t s;
+  int dst;
+  const double* xnew;  // GRAD
+  double* dkg;         // GRAD
+};
+
+template <int MAXL, int M, bool GRAD>
+static hipError_t launch_env_t(const EnvLaunch& a) {
+  if (a.lds > 65536)
+    (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M, GRAD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)a.lds);
+  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs, a.dst,
+                     a.xnew, a.dkg);
   return hipGetLastError();
 }
 
-template <int M>
-static hipError_t launch_env_m(int lines, const Plan* dev, int B, double* kg, double* pairs, dim3 grid, dim3 block,
-                               size_t lds, hipStream_t s, int dst) {
-  if (lines <= 64 * 2) return launch_env_t<2, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
-  if (lines <= 64 * 4) return launch_env_t<4, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
-  if (lines <= 64 * 8) return launch_env_t<8, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
-  if (lines <= 64 * 17) return launch_env_t<17, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
-  if (lines <= 64 * 33) return launch_env_t<33, M>(dev, B, kg, pairs, grid, block, lds, s, dst);
+template <int M, bool GRAD>
+static hipError_t launch_env_m(int lines, const EnvLaunch& a) {
+  if (lines <= 64 * 2) return launch_env_t<2, M, GRAD>(a);
+  if (lines <= 64 * 4) return launch_env_t<4, M, GRAD>(a);
+  if (lines <= 64 * 8) return launch_env_t<8, M, GRAD>(a);
+  if (lines <= 64 * 17) return launch_env_t<17, M, GRAD>(a);
+  if (lines <= 64 * 33) return launch_env_t<33, M, GRAD>(a);
   return hipErrorInvalidValue;
+}
+
+template <bool GRAD>
+static hipError_t launch_env(const Plan& h, const EnvLaunch& a) {
+  switch (outputs_bucket(h.m)) {
+    case 1: return launch_env_m<1, GRAD>(h.N + 1, a);
+    case 2: return launch_env_m<2, GRAD>(h.N + 1, a);
+    case 3: return launch_env_m<3, GRAD>(h.N + 1, a);
+    case 4: return launch_env_m<4, GRAD>(h.N + 1, a);
+    default: return launch_env_m<8, GRAD>(h.N + 1, a);
+  }
 }
 
 // The three launches of one forward on `s`; ev (nullable) gets 4 events
@@ -1034,15 +1412,38 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
       default: return launch_cross_cov_t<16>(h, dev, xnew, B, kg, s, stage);
     }
   }
-  dim3 grid(B, h.split), block(h.sw * WAVE);
-  const size_t lds = envelope_lds_bytes(h.m, h.N, h.sw, h.S);
-  switch (outputs_bucket(h.m)) {
-    case 1: return launch_env_m<1>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
-    case 2: return launch_env_m<2>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
-    case 3: return launch_env_m<3>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
-    case 4: return launch_env_m<4>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
-    default: return launch_env_m<8>(h.N + 1, dev, B, kg, pairs, grid, block, lds, s, h.debug_stamp);
+  EnvLaunch a{dev, B, kg, pairs, dim3(B, h.split), dim3(h.sw * WAVE), envelope_lds_bytes(h.m, h.N, h.sw, h.S), s,
+              h.debug_stamp, nullptr, nullptr};
+  return launch_env<false>(h, a);
+}
+
+template <int DM>
+static hipError_t launch_cross_grad_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* dkg,
+                                      hipStream_t s) {
+  dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m * h.d);
+  const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)cross_grad_plan_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL(cross_grad_plan_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, dkg, 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
+                               hipStream_t s) {
+  hipError_t e;
+  if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 0)) != hipSuccess) return e;  // Q_X, means; kg = 0
+  if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 1)) != hipSuccess) return e;  // cov rows, variances
+  switch (dim_bucket(h.d)) {                                                            // J_g, dmean; dkg = 0
+    case 2: e = launch_cross_grad_t<2>(h, dev, xnew, B, dkg, s); break;
+    case 4: e = launch_cross_grad_t<4>(h, dev, xnew, B, dkg, s); break;
+    case 8: e = launch_cross_grad_t<8>(h, dev, xnew, B, dkg, s); break;
+    default: e = launch_cross_grad_t<16>(h, dev, xnew, B, dkg, s); break;
   }
+  if (e != hipSuccess) return e;
+  EnvLaunch a{dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
+              envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np), s, 0, xnew, dkg};
+  return launch_env<true>(h, a);
 }
 
 hipError_t launch_forward(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,

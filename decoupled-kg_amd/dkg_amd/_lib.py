@@ -15,7 +15,8 @@ from .errors import BotorchTensorDimensionError, DkgNativeError, UnsupportedErro
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdkg.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
+DKG_PLAN_GRAD = 1
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 
@@ -58,9 +59,10 @@ SIGNATURES = {
                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                                   POINTER(c_float)]),
     "dkg_plan_bytes": (c_size_t, []),
-    "dkg_plan_workspace": (c_size_t, [POINTER(DkgOutput), c_int, c_int, c_int, c_int]),
+    "dkg_plan_workspace": (c_size_t, [POINTER(DkgOutput), c_int, c_int, c_int, c_int, c_int, c_int]),
     "dkg_plan_init": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
-                              c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+                              c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+    "dkg_plan_forward_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_plan_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_plan_forward_timed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                        POINTER(c_float)]),

@@ -71,15 +71,23 @@ def _as_model_state(model) -> ModelListGPState:
 
 
 class _ForwardFn(torch.autograd.Function):
-    """Device forward; the closed-form backward is not wired in yet."""
+    """Device forward; when X requires grad the same C call also returns
+    dKG(x_b)/dx_b (dkg_plan_forward_grad), and backward scales it by the
+    incoming gradient.  KG(x_b) depends on x_b only, so the Jacobian is
+    block-diagonal and this is the exact vector-Jacobian product."""
 
     @staticmethod
     def forward(ctx, X, acq):
+        if ctx.needs_input_grad[0]:
+            kg, dkg = acq._plan_for(X.shape[0], grad=True).forward_grad(X)
+            ctx.save_for_backward(dkg)
+            return kg
         return acq._plan_for(X.shape[0]).forward(X)
 
     @staticmethod
-    def backward(ctx, grad):  # pragma: no cover
-        raise NotImplementedError("DiscreteKnowledgeGradient backward (dKG/dX) is not implemented yet")
+    def backward(ctx, grad):
+        (dkg,) = ctx.saved_tensors
+        return grad.to(dkg)[:, None] * dkg, None
 
 
 class DiscreteKnowledgeGradient(_Base):
@@ -132,15 +140,21 @@ class DiscreteKnowledgeGradient(_Base):
         self._state = DeviceGPState(state, x_discretisation, device)
         self._W = scalarisation_weights.detach().to(self._state.device, torch.double).contiguous()
         self._plan = None
+        self._plan_grad = None
 
-    def _plan_for(self, B: int):
-        """The forward plan, grown (powers of two) to hold B candidates."""
-        if self._plan is None or self._plan.max_B < B:
+    def _plan_for(self, B: int, grad: bool = False):
+        """The forward plan (with gradient buffers when ``grad``), grown (powers of two) to hold B candidates."""
+        cur = self._plan_grad if grad else self._plan
+        if cur is None or cur.max_B < B:
             cap = 1
             while cap < B:
                 cap *= 2
-            self._plan = self._state.plan(self._W, self.target_output_ix, max(cap, 16))
-        return self._plan
+            cur = self._state.plan(self._W, self.target_output_ix, max(cap, 16), grad=grad)
+            if grad:
+                self._plan_grad = cur
+            else:
+                self._plan = cur
+        return cur
 
     def set_X_pending(self, X_pending: Optional[Tensor] = None) -> None:
         raise UnsupportedError(f"{type(self).__name__} does not account for X_pending yet.")
@@ -153,7 +167,8 @@ class DiscreteKnowledgeGradient(_Base):
                 f"Expected X to have last dimension matching 'self.x_discretisation'. "
                 f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
         flat = X.reshape(-1, d)
-        kg = _ForwardFn.apply(flat, self)
+        Xd = flat.to(self._state.device, torch.double)
+        kg = _ForwardFn.apply(Xd, self)
         return kg.to(device=X.device, dtype=X.dtype).reshape(batch_shape)
 
     def forward_pairs(self, X: Tensor) -> Tensor:

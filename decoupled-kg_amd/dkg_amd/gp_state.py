@@ -144,8 +144,8 @@ class DeviceGPState:
         self._ws = None
         self._ws_key = None
 
-    def plan(self, W: torch.Tensor, target, max_B: int) -> "ForwardPlan":
-        return ForwardPlan(self, W, target, max_B)
+    def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False) -> "ForwardPlan":
+        return ForwardPlan(self, W, target, max_B, grad)
 
     def forward(self, X: torch.Tensor, W: torch.Tensor, target, kg_pairs=None, timed: bool = False):
         """One-shot forward (builds a plan on the fly); see ForwardPlan for the fast path."""
@@ -156,9 +156,11 @@ class DeviceGPState:
 class ForwardPlan:
     """A DKG plan (include/dkg.h "Plan API"): weights, target and workspace for
     up to ``max_B`` candidates, device copy written once; ``forward`` is one
-    C call that launches the three kernels on the current stream."""
+    C call that launches the three kernels on the current stream.  With
+    ``grad=True`` the workspace also holds the gradient buffers and
+    ``forward_grad`` returns dKG/dx alongside KG."""
 
-    def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int):
+    def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int, grad: bool = False):
         lib = _lib.load()
         self.state = state
         self.device = state.device
@@ -168,13 +170,15 @@ class ForwardPlan:
         self.S = self.W.shape[0]
         self.target = -1 if target is None else int(target)
         self.max_B = int(max_B)
-        need = lib.dkg_plan_workspace(state.structs, state.m, state.N, self.max_B, self.S)
+        self.grad = bool(grad)
+        flags = _lib.DKG_PLAN_GRAD if self.grad else 0
+        need = lib.dkg_plan_workspace(state.structs, state.m, state.d, state.N, self.max_B, self.S, flags)
         self.ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
         nbytes = lib.dkg_plan_bytes()
         self.host = ctypes.create_string_buffer(nbytes)
         self.dev = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         _lib.check(lib.dkg_plan_init(state.structs, state.m, state.d, _lib.ptr(state.D), state.N, _lib.ptr(self.W),
-                                     self.S, self.target, self.max_B, _lib.ptr(self.ws), self.ws.numel(),
+                                     self.S, self.target, self.max_B, flags, _lib.ptr(self.ws), self.ws.numel(),
                                      self.host, _lib.ptr(self.dev), current_stream_ptr(self.device)),
                    "dkg_plan_init")
         self._fwd = lib.dkg_plan_forward
@@ -188,6 +192,21 @@ class ForwardPlan:
                        torch.cuda.current_stream(self.device).cuda_stream)
         if st:
             _lib.check(st, "dkg_plan_forward")
+
+    def forward_grad(self, X: torch.Tensor):
+        """KG[B] and dKG/dx [B, d] for candidates X (B x d): one C call."""
+        if not self.grad:
+            raise ValueError("plan was built without grad=True")
+        X = X.detach().to(self.device, torch.double).contiguous()
+        B = X.shape[0]
+        if B > self.max_B:
+            raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
+        kg = torch.empty(B, dtype=torch.double, device=self.device)
+        dkg = torch.empty(B, self.state.d, dtype=torch.double, device=self.device)
+        _lib.check(_lib.load().dkg_plan_forward_grad(self.host, self._dev_ptr, _lib.ptr(X), B, _lib.ptr(kg),
+                                                     _lib.ptr(dkg), current_stream_ptr(self.device)),
+                   "dkg_plan_forward_grad")
+        return kg, dkg
 
     def time_stage(self, X: torch.Tensor, stage: int, reps: int) -> float:
         """Average duration (ms) of ``reps`` back-to-back launches of one kernel

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 1
+#define DKG_ABI_VERSION 2
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -131,11 +131,13 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
  * size) on `stream`.  dkg_plan_forward then launches the three kernels with a
  * pointer to the device copy (no per-call host-to-device traffic).  The
  * disc/weights/workspace buffers must outlive the plan. */
+/* Plan flags: DKG_PLAN_GRAD adds the gradient buffers (dkg_plan_forward_grad). */
+#define DKG_PLAN_GRAD 1
 size_t dkg_plan_bytes(void);
-size_t dkg_plan_workspace(const dkg_output* outs, int m, int N, int max_B, int S);
+size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags);
 int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
-                  int target, int max_B, void* workspace, size_t workspace_bytes, void* host_plan, void* dev_plan,
-                  void* stream);
+                  int target, int max_B, int flags, void* workspace, size_t workspace_bytes, void* host_plan,
+                  void* dev_plan, void* stream);
 /* kg[b] (and kg_pairs[b x S], nullable) for B <= max_B candidates xnew (device, B x d);
  * same result as dkg_forward with the plan's arguments. */
 int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
@@ -143,6 +145,18 @@ int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* 
 /* As dkg_plan_forward with per-kernel HIP-event timings (synchronises): stage_ms[3]. */
 int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                            double* kg_pairs, void* stream, float* stage_ms);
+/* Value and gradient (plan built with DKG_PLAN_GRAD): kg[b] as dkg_plan_forward
+ * and dkg_dx[b*d + j] = d kg[b] / d xnew[b*d + j] (device, B x d).  Replaces
+ * the autograd backward of DiscreteKnowledgeGradient.forward (discretekg.py:
+ * 131-159; exercised by test_discretekg.py:110-135 and by optimize_acqf,
+ * acquisition_optimisation_strategy.py:217-224, 259-266).  With the upper
+ * envelope fixed (envelope theorem), per scalarisation
+ *   dKG/dx = sum_{envelope lines e} [ (phi(c_L) - phi(c_R)) db_e/dx
+ *                                      + (Phi(c_R) - Phi(c_L)) [e = 0] da_0/dx ]
+ *            - [line 0 attains max a] da_0/dx,
+ * where only the candidate's own line 0 intercept and the slopes depend on x. */
+int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                          double* dkg_dx, void* stream);
 /* Benchmark helper: average HIP-event duration (ms) of `reps` back-to-back
  * launches of one stage (0 cross_root, 1 posterior_cov, 2 envelope) on
  * `stream`, after one full forward that primes its inputs; a final full

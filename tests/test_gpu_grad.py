@@ -1,0 +1,140 @@
+"""dKG/dX through the C ABI (dkg_plan_forward_grad) vs the oracle's autograd.
+
+The reference's forward is differentiable (test_discretekg.py:110-135 runs
+gradcheck on it; optimize_acqf's L-BFGS-B needs dKG/dX).  The oracle is the
+structure-faithful restatement; torch.autograd through it is the gradient
+reference (its own gradcheck passes in test_oracle_kats.py).
+
+Tolerance: |g - g_ref| <= 1e-6 |g_ref| + 1e-9 * max|g_ref| over the batch,
+per coordinate (the absolute term is the rounding floor of the envelope sums
+relative to the largest gradient in the batch).
+"""
+
+import pytest
+import torch
+
+from dkg_amd import DiscreteKnowledgeGradient
+from dkg_amd.synthetic import WORKLOADS, make_problem
+from helpers import load_golden, to_oracle
+from oracle.discretekg import discrete_kg_batched
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def oracle_grad(om, X, D, W, target):
+    Xr = X.clone().requires_grad_(True)
+    kg, _ = discrete_kg_batched(om, Xr, D, W, target)
+    (g,) = torch.autograd.grad(kg.sum(), Xr)
+    return kg.detach(), g
+
+
+def native_grad(state, X, D, W, target):
+    acq = DiscreteKnowledgeGradient(state, D, W, target_output_ix=target, device=DEV)
+    Xr = X.clone().to(DEV).requires_grad_(True)
+    kg = acq(Xr.unsqueeze(-2))
+    (g,) = torch.autograd.grad(kg.sum(), Xr)
+    return kg.detach().cpu(), g.cpu()
+
+
+def assert_grad_close(g, ref):
+    floor = 1e-9 * ref.abs().max().clamp_min(1e-300)
+    err = (g - ref).abs()
+    tol = 1e-6 * ref.abs() + floor
+    assert bool((err <= tol).all()), f"max err {err.max():.3e}, worst ratio {(err / tol).max():.3f}"
+
+
+@pytest.mark.parametrize("workload", ["small", "parity6d"])
+@pytest.mark.parametrize("target", [None, 0, 1])
+def test_grad_vs_oracle(workload, target):
+    w = WORKLOADS[workload]
+    model, D, X, W = make_problem(w)
+    X, W = X[:12], W[:8]
+    om = to_oracle(model)
+    kg_ref, g_ref = oracle_grad(om, X, D, W, target)
+    kg, g = native_grad(model, X, D, W, target)
+    assert g.shape == X.shape
+    assert_grad_close(g, g_ref)
+
+
+@pytest.mark.parametrize("name", ["lengthscales0", "observationnoise0"])
+@pytest.mark.parametrize("target", [None, 1])
+def test_grad_golden_problems(name, target):
+    state, om, D, W, X, _ = load_golden(name)
+    X = X[:10]
+    _, g_ref = oracle_grad(om, X, D, W, target)
+    _, g = native_grad(state, X, D, W, target)
+    assert_grad_close(g, g_ref)
+
+
+def test_grad_matches_central_differences():
+    """The analytic device gradient against central differences of the device forward."""
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    X = X[:6]
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    Xr = X.clone().to(DEV).requires_grad_(True)
+    (g,) = torch.autograd.grad(acq(Xr.unsqueeze(-2)).sum(), Xr)
+    h = 1e-6
+    fd = torch.zeros_like(X)
+    for j in range(X.shape[1]):
+        e = torch.zeros_like(X)
+        e[:, j] = h
+        up = acq((X + e).to(DEV).unsqueeze(-2)).cpu()
+        dn = acq((X - e).to(DEV).unsqueeze(-2)).cpu()
+        fd[:, j] = (up - dn) / (2 * h)
+    torch.testing.assert_close(g.cpu(), fd, rtol=1e-4, atol=1e-7 * fd.abs().max().item())
+
+
+def test_grad_headline_batch_consistent():
+    """Headline-size batch: gradient rows equal those of the same candidates evaluated alone."""
+    model, D, X, W = make_problem(WORKLOADS["headline"])
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    Xr = X.clone().to(DEV).requires_grad_(True)
+    kg = acq(Xr.unsqueeze(-2))
+    (g,) = torch.autograd.grad(kg.sum(), Xr)
+    kg_plain = acq(X.to(DEV).unsqueeze(-2))
+    # same KG with and without the gradient path (edge sums in a different order: rounding only)
+    torch.testing.assert_close(kg.detach(), kg_plain, rtol=1e-12, atol=1e-300)
+    Xs = X[:5].clone().to(DEV).requires_grad_(True)
+    (gs,) = torch.autograd.grad(acq(Xs.unsqueeze(-2)).sum(), Xs)
+    assert torch.equal(gs, g[:5])
+
+
+def test_grad_flows_with_batch_shape_and_weights():
+    """[*batch, 1, d] input and a weighted sum of outputs backpropagate exactly."""
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    Xb = X[:6].reshape(2, 3, 1, 2).clone().to(DEV).requires_grad_(True)
+    wts = torch.arange(1.0, 7.0, dtype=torch.double, device=DEV).reshape(2, 3)
+    (g,) = torch.autograd.grad((acq(Xb) * wts).sum(), Xb)
+    X0 = X[:6].clone().to(DEV).requires_grad_(True)
+    (g0,) = torch.autograd.grad(acq(X0.unsqueeze(-2)).sum(), X0)
+    torch.testing.assert_close(g.reshape(6, 2), g0 * wts.reshape(6, 1), rtol=0, atol=0)
+
+
+# test_discretekg.py:110-135 through the device path: gradcheck of the module
+# functions at xnew = (0.51, 0.51) on the reference test models.
+@pytest.fixture(scope="module")
+def ref_models():
+    from oracle.fit import make_reference_test_model, reference_test_discretisation
+
+    return {True: make_reference_test_model(use_noise=True), False: make_reference_test_model(use_noise=False),
+            "disc": reference_test_discretisation()}
+
+
+@pytest.mark.parametrize("noisy", [True, False], ids=["noisy", "noiseless"])
+@pytest.mark.parametrize("weights", [[[0.6, 0.4]], [[0.7, 0.3], [0.6, 0.4], [0.5, 0.5]]], ids=["single", "trio"])
+@pytest.mark.parametrize("target", [None, 0, 1])
+def test_reference_gradcheck(ref_models, noisy, weights, target):
+    from dkg_amd import calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output
+    from helpers import to_state
+
+    state = to_state(ref_models[noisy])
+    disc = ref_models["disc"]
+    W = torch.tensor(weights, dtype=torch.double)
+    xnew = torch.tensor([0.51, 0.51], dtype=torch.double, device=DEV, requires_grad=True)
+    if target is None:
+        fn = lambda x: calculate_discrete_kg(state, x, disc, W)  # noqa: E731
+    else:
+        fn = lambda x: calculate_discrete_kg_conditioning_on_single_output(state, x, target, disc, W)  # noqa: E731
+    assert torch.autograd.gradcheck(fn, (xnew,), raise_exception=True)
