@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-reps", type=int, default=50)
+    ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_headline.json"),
                     help="per-kernel HBM traffic from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
     return ap.parse_args()
@@ -190,6 +191,20 @@ def main():
             "avg_launch_us": avg_ms[dom] * 1e3,
             "stages_us": {n: a * 1e3 for n, a in zip(names, avg_ms)}}
 
+    # ---- value + gradient (dkg_plan_forward_grad: the optimize_acqf L-BFGS-B path), same batch
+    grad_info = None
+    if args.grad_steps > 0:
+        gplan = acq._plan_for(w.B, grad=True)
+        for _ in range(3):
+            gplan.forward_grad(Xd)
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(args.grad_steps):
+            gplan.forward_grad(Xd)
+        torch.cuda.synchronize()
+        gdt = (time.perf_counter() - g0) / args.grad_steps
+        grad_info = {"value": w.B / gdt, "unit": "KG-evals+gradients/s (per GPU)", "ms_per_step": gdt * 1e3}
+
     out = None
     if rank == 0:
         cpu = None
@@ -215,6 +230,7 @@ def main():
                        "parallelism": f"{args.shard} sharded over {world} GPU(s); per-step async "
                                       f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'}"},
             "forward_calls_per_s": world * args.steps / elapsed,
+            "value_and_grad": grad_info,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
