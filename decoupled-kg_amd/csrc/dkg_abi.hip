@@ -13,6 +13,7 @@ using namespace dkg;
 namespace {
 
 thread_local std::string g_err;
+unsigned long long* g_kstamps_buf = nullptr;  // debug phase stamps (allocated on first use, kept)
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -97,18 +98,26 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   if (max_B < 0 || N < 0) return fail(DKG_ERR_ARG, "negative size B=%d N=%d", max_B, N);
   if (S < 1) return fail(DKG_ERR_ARG, "S=%d scalarisations", S);
   if (target < -1 || target >= m) return fail(DKG_ERR_ARG, "target_output_ix=%d out of range for %d outputs", target, m);
-  if (N + 1 > 64 * 33) return fail(DKG_ERR_UNSUPPORTED, "N=%d discretisation points (supported <= %d)", N, 64 * 33 - 1);
+  if (N > (1 << 22)) return fail(DKG_ERR_UNSUPPORTED, "N=%d discretisation points (supported <= %d)", N, 1 << 22);
   int sw, split;
   envelope_geometry(std::max(max_B, 1), S, &sw, &split);
-  if (envelope_lds_bytes(m, N, sw, S) > 160 * 1024)
-    return fail(DKG_ERR_UNSUPPORTED, "m=%d outputs x N=%d points exceed the envelope stage's LDS staging", m, N);
+  int max_np = 16;
+  for (int i = 0; i < m; ++i) max_np = std::max(max_np, pad16(outs[i].n));
+  // the envelope stages the line data in LDS when it fits and the lines fit
+  // the register slots; otherwise it streams them from global memory
+  const bool want_grad = (flags & DKG_PLAN_GRAD) != 0;
+  bool stream = N + 1 > 64 * 33 || envelope_lds_bytes(m, N, sw, S, false) > 160 * 1024 ||
+                (want_grad && envelope_grad_lds_bytes(m, N, sw, S, d, max_np, false) > 160 * 1024);
+  if (envelope_lds_bytes(m, N, sw, S, true) > 160 * 1024)
+    return fail(DKG_ERR_UNSUPPORTED, "S=%d x m=%d weights exceed the envelope stage's LDS", S, m);
   if (!weights || !workspace || (N > 0 && !disc)) return fail(DKG_ERR_ARG, "NULL data pointer");
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
   if (flags & ~DKG_PLAN_GRAD) return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
-  if ((flags & DKG_PLAN_GRAD) && envelope_grad_lds_bytes(m, N, sw, S, d, 16) > 160 * 1024)
-    return fail(DKG_ERR_UNSUPPORTED, "gradient: m=%d outputs, N=%d, d=%d exceed the envelope stage's LDS", m, N, d);
+  if (want_grad && envelope_grad_lds_bytes(m, N, sw, S, d, max_np, true) > 160 * 1024)
+    return fail(DKG_ERR_UNSUPPORTED, "gradient: m=%d outputs, n=%d, d=%d exceed the envelope stage's LDS", m, max_np,
+                d);
   const WsLayout L = layout(outs, m, N, max_B, S, d, flags);
   if (workspace_bytes < L.total)
     return fail(DKG_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, L.total);
@@ -125,7 +134,8 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->split = split;
   P->disc = (N > 0) ? disc : reinterpret_cast<const double*>(ws);  // always a readable address
   P->weights = weights;
-  P->grad = (flags & DKG_PLAN_GRAD) ? 1 : 0;
+  P->grad = want_grad ? 1 : 0;
+  P->stream = stream ? 1 : 0;
   P->bpad = pad16(std::max(max_B, 1));
   for (int i = 0; i < m; ++i) {
     P->o[i] = outs[i];
@@ -147,9 +157,12 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
   static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
   P->debug_stamp = dst ? std::atoi(dst) : 0;
-  if (P->grad && envelope_grad_lds_bytes(m, N, sw, S, d, P->max_np) > 160 * 1024)
-    return fail(DKG_ERR_UNSUPPORTED, "gradient: n=%d training points, d=%d exceed the envelope stage's LDS",
-                P->max_np, d);
+  if (P->debug_stamp) {
+    if (!g_kstamps_buf &&
+        hip_check(hipMalloc(&g_kstamps_buf, sizeof(unsigned long long) * 3 * KST_WG * 8), "hipMalloc(stamps)"))
+      return DKG_ERR_HIP;
+    P->kstamps = g_kstamps_buf;
+  }
   return DKG_OK;
 }
 
@@ -339,11 +352,11 @@ int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, d
 }
 
 int dkg_debug_read_kstamps(unsigned long long* host, int n) {
-  return hip_check(read_kstamps(host, n), "hipMemcpyFromSymbol");
-}
-
-int dkg_debug_read_stamps(unsigned long long* host, int n) {
-  return hip_check(read_stamps(host, n), "hipMemcpyFromSymbol");
+  if (!host || n < 0) return fail(DKG_ERR_ARG, "bad arguments");
+  if (!g_kstamps_buf) return fail(DKG_ERR_ARG, "no plan was built with DKG_DEBUG_STAMPS=1");
+  const size_t words = std::min<size_t>((size_t)n, (size_t)3 * KST_WG * 8);
+  return hip_check(hipMemcpy(host, g_kstamps_buf, words * sizeof(unsigned long long), hipMemcpyDeviceToHost),
+                   "hipMemcpy(stamps)");
 }
 
 int dkg_debug_wave_ops(const double* in, double* out, void* stream) {

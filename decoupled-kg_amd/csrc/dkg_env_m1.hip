@@ -1,0 +1,10 @@
+// envelope_kernel instantiations for output bucket M = 1 (forward and gradient).
+#include "dkg_device.h"
+
+namespace dkg {
+
+hipError_t launch_env_m1(bool grad, int lines, bool stream, const EnvLaunch& a) {
+  return grad ? launch_env_bucket<1, true>(lines, stream, a) : launch_env_bucket<1, false>(lines, stream, a);
+}
+
+}  // namespace dkg

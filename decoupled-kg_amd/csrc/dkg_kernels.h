@@ -18,6 +18,8 @@ struct Plan {
   int32_t debug_stamp;              // 1: per-workgroup phase stamps into g_kstamps (0 in production)
   int32_t grad;                     // workspace holds the gradient buffers (DKG_PLAN_GRAD)
   int32_t bpad;                     // pad16(max_B): rows of the fragment-packed candidate buffers
+  int32_t stream;                   // envelope streams the lines from global memory (large N)
+  int32_t pad2_;
   const double* disc;               // [N x d]
   const double* weights;            // [S x m]
   double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
@@ -26,6 +28,7 @@ struct Plan {
   double* cov[DKG_MAX_OUTPUTS];     // [B x N] posterior covariance rows per output (workspace)
   double* jq[DKG_MAX_OUTPUTS];      // GRAD: d fragment-packed dK(x,X)/dx_g R matrices (bpad x n_pad each)
   double* gmu[DKG_MAX_OUTPUTS];     // GRAD: [d][bpad] model-space mean gradients
+  unsigned long long* kstamps;      // debug_stamp: [3][KST_WG][8] phase stamps (device)
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
   int* tickets;                     // [B] arrival counters (split > 2 only)
 };
@@ -46,24 +49,22 @@ hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
 // Value and gradient: kg[B] and dkg[B x d] (d KG(x_b) / d x_b), plan built with DKG_PLAN_GRAD.
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
                                hipStream_t s);
-size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np);
+size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream);
 // One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                         hipStream_t s, int stage);
 hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                           hipStream_t s, hipEvent_t* ev);
 hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s);
-hipError_t read_stamps(unsigned long long* host, int n);
 // Per-workgroup phase stamps of the forward kernels: [3 kernels][KST_WG][8].
 constexpr int KST_WG = 1024;
-hipError_t read_kstamps(unsigned long long* host, int n);
 hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s);
 hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStream_t s);
 
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and
 // workgroups per candidate.
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split);
-size_t envelope_lds_bytes(int m, int N, int waves, int S);
+size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream);
 size_t cross_root_lds_bytes(int np, int d);
 
 }  // namespace dkg

@@ -46,7 +46,10 @@ WORKLOADS = {
     "headline": Workload("headline", m=2, n_train=256, grid=32, S=16, B=128),
     # well-conditioned, non-degenerate parity variant
     "parity6d": Workload("parity6d", m=2, n_train=128, grid=3, S=8, B=32, d=6,
-                         lengthscales=(0.5, 0.5), outputscales=(1.0, 1.0), noise=1e-2),
+                         lengthscales=(0.4, 0.7), outputscales=(1.0, 3.0), noise=1e-2),
+    # BASELINE.json configs[4] (the stress config; computed in fp64 here)
+    "stress": Workload("stress", m=3, n_train=1024, grid=64, S=32, B=256,
+                       lengthscales=(0.2, 1.8, 0.6), outputscales=(1.0, 50.0, 5.0), noise=1e-3),
 }
 
 

@@ -173,9 +173,6 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
 int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,
                  void* stream);
 
-/* Debug: copy the envelope kernel's phase stamps (written when the env var
- * DKG_DEBUG_ENV_FLAGS has bit 4 set at plan creation) to host memory: n words. */
-int dkg_debug_read_stamps(unsigned long long* host, int n);
 /* Debug: per-workgroup phase stamps of the three forward kernels, written when
  * the env var DKG_DEBUG_STAMPS=1 at plan creation: [3][1024][8] words (slot 0
  * s_memrealtime at start, 1..6 s_memtime at phase boundaries, 7 s_memrealtime

@@ -318,3 +318,21 @@ def test_wave_butterfly_primitives():
         assert torch.equal(o[s], x[p]), f"step {s}: got lanes {((o[s] - 1) / 3).long().tolist()}"
     assert torch.equal(o[6], torch.full((64,), float(x.sum()), dtype=torch.double))
     assert torch.equal(o[7], torch.full((64,), float(x.max()), dtype=torch.double))
+
+
+# ---------------------------------------------------------------- stress sizes
+@pytest.mark.parametrize("target", [None, 2])
+def test_stress_config_parity(target):
+    """BASELINE.json configs[4] shape (m=3, n=1024, N=4096 = 64^2 grid, S=32), fp64:
+    the envelope streams its 4097 lines per pair from global memory."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["stress"])
+    X = X[:4]
+    om = to_oracle(model)
+    ref, _ = discrete_kg_batched(om, X, D, W, target)
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    assert acq._plan_for(4).state is not None
+    got = acq(X.to(DEV).unsqueeze(-2)).cpu()
+    assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
