@@ -39,6 +39,7 @@ struct WsLayout {
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
   size_t cov[DKG_MAX_OUTPUTS];
+  size_t mux_all, var_all, cov_all, mu_all;
   size_t wg_part;
   size_t tickets;
   size_t total;
@@ -57,12 +58,22 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
     }
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
-    L.mux[i] = off;
-    off = align256(off + Bp * sizeof(double));
-    L.var[i] = off;
-    off = align256(off + Bp * sizeof(double));
-    L.cov[i] = off;
-    off = align256(off + (size_t)std::max(B, 1) * std::max(N, 1) * sizeof(double));
+  }
+  // contiguous per-output blocks (the envelope stage addresses them from
+  // kernel-argument base pointers): means and variances at the candidates
+  // [m][Bp], the covariance rows [m][B][N], a copy of mu_D [m][N]
+  L.mux_all = off;
+  off = align256(off + (size_t)m * Bp * sizeof(double));
+  L.var_all = off;
+  off = align256(off + (size_t)m * Bp * sizeof(double));
+  L.cov_all = off;
+  off = align256(off + (size_t)m * std::max(B, 1) * std::max(N, 1) * sizeof(double));
+  L.mu_all = off;
+  off = align256(off + (size_t)m * std::max(N, 1) * sizeof(double));
+  for (int i = 0; i < m; ++i) {
+    L.mux[i] = L.mux_all + (size_t)i * Bp * sizeof(double);
+    L.var[i] = L.var_all + (size_t)i * Bp * sizeof(double);
+    L.cov[i] = L.cov_all + (size_t)i * std::max(B, 1) * std::max(N, 1) * sizeof(double);
   }
   int sw, split;
   envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split);
@@ -149,6 +160,11 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
     P->var[i] = reinterpret_cast<double*>(ws + L.var[i]);
     P->cov[i] = reinterpret_cast<double*>(ws + L.cov[i]);
   }
+  P->mux_all = reinterpret_cast<double*>(ws + L.mux_all);
+  P->var_all = reinterpret_cast<double*>(ws + L.var_all);
+  P->cov_all = reinterpret_cast<double*>(ws + L.cov_all);
+  P->mu_all = reinterpret_cast<double*>(ws + L.mu_all);
+  P->cov_stride = (int64_t)std::max(max_B, 1) * std::max(N, 1);
   P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
   static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
@@ -189,6 +205,16 @@ int run_forward(const Plan& h, const Plan* dev, const double* xnew, int B, doubl
 
 size_t plan_slot_bytes() { return align256(sizeof(Plan)); }
 
+// mu_D of every output into the plan's contiguous [m][N] block (stream ordered).
+int copy_disc_means(const Plan& P, hipStream_t s) {
+  for (int i = 0; i < P.m && P.N > 0; ++i) {
+    const int st = hip_check(hipMemcpyAsync(P.mu_all + (size_t)i * P.N, P.o[i].disc_mean, sizeof(double) * P.N,
+                                            hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(mu_D)");
+    if (st) return st;
+  }
+  return DKG_OK;
+}
+
 // One-shot path: plan built on the host per call, its device copy placed in
 // the workspace tail (one small host-to-device copy per call).
 int forward_oneshot(const dkg_output* outs, int m, int d, const double* disc, int N, const double* xnew, int B,
@@ -200,6 +226,7 @@ int forward_oneshot(const dkg_output* outs, int m, int d, const double* disc, in
   thread_local Plan h;
   int st = build_plan(outs, m, d, disc, N, weights, S, target, B, workspace, avail, &h);
   if (st) return st;
+  if ((st = copy_disc_means(h, stream))) return st;
   Plan* dev = reinterpret_cast<Plan*>((reinterpret_cast<uintptr_t>(workspace) + avail + 255) & ~(uintptr_t)255);
   if ((st = hip_check(hipMemcpyAsync(dev, &h, sizeof(Plan), hipMemcpyHostToDevice, stream), "hipMemcpyAsync")))
     return st;
@@ -309,6 +336,7 @@ int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int 
   Plan* h = static_cast<Plan*>(host_plan);
   int st = build_plan(outs, m, d, disc, N, weights, S, target, max_B, workspace, workspace_bytes, h, flags);
   if (st) return st;
+  if ((st = copy_disc_means(*h, (hipStream_t)stream))) return st;
   return hip_check(hipMemcpyAsync(dev_plan, h, sizeof(Plan), hipMemcpyHostToDevice, (hipStream_t)stream),
                    "hipMemcpyAsync");
 }

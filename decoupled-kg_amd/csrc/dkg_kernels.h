@@ -29,6 +29,11 @@ struct Plan {
   double* jq[DKG_MAX_OUTPUTS];      // GRAD: d fragment-packed dK(x,X)/dx_g R matrices (bpad x n_pad each)
   double* gmu[DKG_MAX_OUTPUTS];     // GRAD: [d][bpad] model-space mean gradients
   unsigned long long* kstamps;      // debug_stamp: [3][KST_WG][8] phase stamps (device)
+  double* mux_all;                  // [m][bpad]  = mux[0..m)
+  double* var_all;                  // [m][bpad]  = var[0..m)
+  double* cov_all;                  // [m][cov_stride] = cov[0..m)
+  double* mu_all;                   // [m][N] copy of the outputs' disc_mean
+  int64_t cov_stride;               // max_B * N
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
   int* tickets;                     // [B] arrival counters (split > 2 only)
 };

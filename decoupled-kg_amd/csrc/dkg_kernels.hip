@@ -537,7 +537,7 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
       default: return launch_cross_cov_t<16>(h, dev, xnew, B, kg, s, stage);
     }
   }
-  EnvLaunch a{dev, B, kg, pairs, dim3(B, h.split), dim3(h.sw * WAVE),
+  EnvLaunch a{&h, dev, B, kg, pairs, dim3(B, h.split), dim3(h.sw * WAVE),
               envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0), s, h.debug_stamp, nullptr, nullptr};
   return launch_env<false>(h, a);
 }
@@ -566,7 +566,7 @@ hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xne
     default: e = launch_cross_grad_t<16>(h, dev, xnew, B, dkg, s); break;
   }
   if (e != hipSuccess) return e;
-  EnvLaunch a{dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
+  EnvLaunch a{&h, dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
               envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, 0, xnew, dkg};
   return launch_env<true>(h, a);
 }

@@ -20,10 +20,14 @@ PATHS = [("full", None), ("t0", 0), ("t1", 1)]
 @pytest.mark.parametrize("name", NAMES)
 def test_oracle_reproduces_golden(name):
     _, om, D, W, X, t = load_golden(name)
-    for i in (0, 5, 17):
-        torch.testing.assert_close(calculate_discrete_kg(om, X[i], D, W), t["kg_full"][i], rtol=1e-12, atol=1e-15)
-        torch.testing.assert_close(calculate_discrete_kg_conditioning_on_single_output(om, X[i], 1, D, W),
-                                   t["kg_t1"][i], rtol=1e-12, atol=1e-15)
+    # the generating machine's BLAS may sum in another order: the suite's KG tolerance
+    idx = torch.tensor([0, 5, 17])
+    floor_full = rounding_floor(om, X[idx], D, W, None)
+    floor_t1 = rounding_floor(om, X[idx], D, W, 1)
+    got_full = torch.stack([calculate_discrete_kg(om, X[i], D, W) for i in idx])
+    got_t1 = torch.stack([calculate_discrete_kg_conditioning_on_single_output(om, X[i], 1, D, W) for i in idx])
+    assert_kg_close(got_full, t["kg_full"][idx], floor_full)
+    assert_kg_close(got_t1, t["kg_t1"][idx], floor_t1)
     a, b = lines_batched(om, X[:4], D, W, None)
     torch.testing.assert_close(a, t["lines_a"], rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(b, t["lines_b"], rtol=1e-12, atol=1e-12)
