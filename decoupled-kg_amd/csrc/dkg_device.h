@@ -200,22 +200,17 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
   }
   f.cnt = cnt;
   f.status = (cnt + 3 > ENV_CAP) ? 2 : 0;
-  if constexpr (IDX) {
-    f.kL = wave_first_index<MAXL>(lane, [&](int t) { return lb[t] == bL && la[t] == aL; });
-    f.kT = wave_first_index<MAXL>(lane, [&](int t) { return la[t] == aT && lb[t] == bT; });
-    f.kR = wave_first_index<MAXL>(lane, [&](int t) { return lb[t] == bR && la[t] == aR; });
-    int c = 0;
-#pragma unroll
-    for (int t = 0; t < MAXL; ++t) c += __popcll(__ballot(la[t] == aT));
-    f.cntT = c;
-  }
+  // IDX: the line indices of L, T, R and the count of max-a lines are
+  // resolved lazily by the caller (rarely needed; keeps register pressure low)
+  f.kL = f.kT = f.kR = -1;
+  f.cntT = -1;
   return f;
 }
 
 // Exact upper envelope of the candidate list (survivors + L, T, R) and the
 // cancellation-free expectation; needs no register lines.
 __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, double* sb, double* sa, int* nhull,
-                                                int dbg = 0) {
+                                                int /*unused*/ = 0) {
   const int cnt = f.cnt;
   const double bT = f.bT;
   if (lane == 0) {
@@ -227,7 +222,6 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (dbg & 1024) return sb[lane & 7];  // ablation: list only
   // ---- right neighbour of every candidate P (one per lane, two chunks of 64
   // at most): the line that takes over from P as z grows, i.e. the reference
   // walk's step (discretekg.py:382-401): argmin over b_Q > b_P of the
@@ -266,7 +260,6 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
     nxt[c] = rj; cn[c] = rn; cd[c] = rd; cb[c] = rb; pb[c] = bP;
   }
 
-  if (dbg & 2048) return cn[0] + cd[1] + (double)nxt[0];  // ablation: + right neighbours
   // ---- follow the chain from L (index cnt): its members are the envelope
   // lines in increasing slope, ending at R (no right neighbour).
   uint64_t on0 = 0, on1 = 0;
@@ -276,7 +269,6 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
     ++h;
     cur = (cur < 64) ? __builtin_amdgcn_readlane(nxt[0], cur) : __builtin_amdgcn_readlane(nxt[1], cur - 64);
   }
-  if (dbg & 4096) return (double)(on0 + on1) + cn[0];  // ablation: + chain walk
   // ---- each envelope line other than R contributes its right edge P -> Q:
   //   (b_Q - b_P) psi(+-c), minus sign when the edge ends at or left of T.
   double v = 0.0;
@@ -287,7 +279,7 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
     if (on && nxt[c] >= 0) {
       const double cc = cn[c] / cd[c];
       const double sc = (cb[c] <= bT) ? -cc : cc;
-      v += (cb[c] - pb[c]) * ((dbg & 64) ? sc * sc : psi(sc));  // 64: ablation, psi -> c^2
+      v += (cb[c] - pb[c]) * psi(sc);
     }
   }
   if (nhull) *nhull = h;
@@ -301,9 +293,9 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
 // visit(k, b, a, cL, cR); the return value is KG_w as in the forward.
 
 // From the candidate list of an IDX filter (si holds the line indices).
-template <class Visit>
+template <class Visit, class Resolve>
 __device__ __forceinline__ double envelope_hull_visit(const EnvFilter& f, int lane, double* sb, double* sa, int* si,
-                                                      Visit&& visit) {
+                                                      Visit&& visit, Resolve&& resolve) {
   const int cnt = f.cnt;
   const double bT = f.bT;
   if (lane == 0) {
@@ -355,7 +347,8 @@ __device__ __forceinline__ double envelope_hull_visit(const EnvFilter& f, int la
     const int ln = cur & 63;
     const double bP = readlane_f64(hi ? lb_[1] : lb_[0], ln);
     const double aP = readlane_f64(hi ? la_[1] : la_[0], ln);
-    const int kP = __builtin_amdgcn_readlane(hi ? li_[1] : li_[0], ln);
+    int kP = __builtin_amdgcn_readlane(hi ? li_[1] : li_[0], ln);
+    if (kP < 0) kP = resolve(bP, aP);  // L, T or R: find its line index
     const int nx = __builtin_amdgcn_readlane(hi ? nxt[1] : nxt[0], ln);
     double cR = INFINITY;
     if (nx >= 0) {
@@ -372,11 +365,12 @@ __device__ __forceinline__ double envelope_hull_visit(const EnvFilter& f, int la
 }
 
 // Gift wrap over register lines with the line index carried (list overflow).
-template <int MAXL, class Visit>
+template <int MAXL, class Visit, class Resolve>
 __device__ __forceinline__ double envelope_walk_visit(const double (&la)[MAXL], const double (&lb)[MAXL], int nl,
-                                                      int lane, const EnvFilter& f, Visit&& visit) {
+                                                      int lane, const EnvFilter& f, Visit&& visit,
+                                                      Resolve&& resolve) {
   double bc = f.bL, ac = f.aL, kg = 0.0, cL = -INFINITY;
-  int kc = f.kL;
+  int kc = resolve(f.bL, f.aL);
   for (int guard = 0; guard <= nl; ++guard) {
     if (!uniform(bc < f.bR)) break;
     double bn = INFINITY, bd = 1.0, bbest = -INFINITY, abest = -INFINITY;
@@ -492,37 +486,17 @@ __device__ __forceinline__ EnvFilter envelope_filter_stream(int nch, int lane, d
   }
   f.cnt = cnt;
   f.status = (cnt + 3 > ENV_CAP) ? 2 : 0;
-  if constexpr (IDX) {
-    int kL = 1 << 30, kT = 1 << 30, kR = 1 << 30, ct = 0;
-    for (int c = nch - 1; c >= 0; --c) {
-      double la[MAXL], lb[MAXL];
-      build(c, la, lb);
-#pragma unroll
-      for (int t = MAXL - 1; t >= 0; --t) {
-        const int k = c * 64 * MAXL + lane + 64 * t;
-        kL = (lb[t] == bL && la[t] == aL) ? k : kL;
-        kT = (la[t] == aT && lb[t] == bT) ? k : kT;
-        kR = (lb[t] == bR && la[t] == aR) ? k : kR;
-        ct += __popcll(__ballot(la[t] == aT));
-      }
-    }
-    DKG_BUTTERFLY({
-      const int st = S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32;
-      kL = min(kL, __shfl_xor(kL, st));
-      kT = min(kT, __shfl_xor(kT, st));
-      kR = min(kR, __shfl_xor(kR, st));
-    })
-    f.kL = kL; f.kT = kT; f.kR = kR; f.cntT = ct;
-  }
+  f.kL = f.kT = f.kR = -1;
+  f.cntT = -1;
   return f;
 }
 
 // Gift wrap over streamed lines (list overflow), index carried; visit may be a no-op.
 template <int MAXL, class Build, class Visit>
 __device__ __forceinline__ double envelope_walk_stream(int nch, int nl, int lane, const EnvFilter& f, Build&& build,
-                                                       Visit&& visit) {
+                                                       Visit&& visit, int kL) {
   double bc = f.bL, ac = f.aL, kg = 0.0, cL = -INFINITY;
-  int kc = f.kL;
+  int kc = kL;
   for (int guard = 0; guard <= nl; ++guard) {
     if (!uniform(bc < f.bR)) break;
     double bn = INFINITY, bd = 1.0, bbest = -INFINITY, abest = -INFINITY;
@@ -633,7 +607,6 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   const int NL = N + 1;
   const int S = P->S;
   const int target = P->target;
-  const int dbg = P->debug_env;
   const bool full = target < 0;
   const int SL = STREAM ? 0 : stage_len(N);
   unsigned long long* st = kst_slot(dst, P, 2);
@@ -690,7 +663,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   const double* wsrc = wts;
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    if (!STREAM && i < m && !(dbg & 8)) {
+    if (!STREAM && i < m) {
       dma_to_lds(mu_src[i], lmu + (size_t)i * SLp, N, wave, SW, lane);
       if (full || i == target) dma_to_lds(cv_src[i], lcv + (size_t)i * SLp, N, wave, SW, lane);
     }
@@ -939,49 +912,72 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
               }
               const double coef = Dw * wb[i];
               const double hc = coef * os[i] * kernel_dprofile(o.kernel, r2);
-              // J_i^T Q_D,i[k-1]: lanes over the training columns, one butterfly for all coordinates
+              // J_i^T Q_D,i[k-1]: lanes over the training columns, one coordinate at a time
               const int npi = pad16(o.n), KBi = npi / 4, r = k - 1;
-              double dot[DKG_MAX_DIM];
-#pragma unroll
-              for (int dd = 0; dd < DKG_MAX_DIM; ++dd) dot[dd] = 0.0;
-              for (int c = lane; c < npi; c += 64) {
-                const double qd = o.disc_frag[frag_index(r >> 4, c >> 2, ((c & 3) << 4) | (r & 15), KBi)];
-#pragma unroll
-                for (int dd = 0; dd < DKG_MAX_DIM; ++dd)
-                  if (dd < d) dot[dd] = fma(jrow[((size_t)i * d + dd) * NP + c], qd, dot[dd]);
-              }
-              auto bfly = [&](auto step) {
-                constexpr int S_ = decltype(step)::value;
-#pragma unroll
-                for (int dd = 0; dd < DKG_MAX_DIM; ++dd)
-                  if (dd < d) dot[dd] += partner_f64<S_>(dot[dd]);
-              };
-              bfly(std::integral_constant<int, 0>{});
-              bfly(std::integral_constant<int, 1>{});
-              bfly(std::integral_constant<int, 2>{});
-              bfly(std::integral_constant<int, 3>{});
-              bfly(std::integral_constant<int, 4>{});
-              bfly(std::integral_constant<int, 5>{});
-              if (lane == 0)
-                for (int dd = 0; dd < d; ++dd) {
+              for (int dd = 0; dd < d; ++dd) {
+                double acc = 0.0;
+                for (int c = lane; c < npi; c += 64)
+                  acc = fma(jrow[((size_t)i * d + dd) * NP + c],
+                            o.disc_frag[frag_index(r >> 4, c >> 2, ((c & 3) << 4) | (r & 15), KBi)], acc);
+                acc = wave_sum(acc);
+                if (lane == 0) {
                   const double il = o.inv_lengthscale[dd];
-                  gw[dd] += hc * (sx[dd] - z[dd]) * il * il - coef * dot[dd];
+                  gw[dd] += hc * (sx[dd] - z[dd]) * il * il - coef * acc;
                 }
+              }
             }
           }
         }
       };
+      // line indices of L, T, R (lowest among exact duplicates) and the number
+      // of lines attaining max a: one pass over the rebuilt lines, after the
+      // filter has released its registers
+      if (f.status != 1) {
+        int kL = 1 << 30, kT = 1 << 30, kR = 1 << 30, ct = 0;
+        auto scan = [&](const double (&la)[MAXL], const double (&lb)[MAXL], int base) {
+#pragma unroll
+          for (int t = MAXL - 1; t >= 0; --t) {
+            const int k = base + lane + 64 * t;
+            kL = (lb[t] == f.bL && la[t] == f.aL) ? k : kL;
+            kT = (la[t] == f.aT && lb[t] == f.bT) ? k : kT;
+            kR = (lb[t] == f.bR && la[t] == f.aR) ? k : kR;
+            ct += __popcll(__ballot(la[t] == f.aT));
+          }
+        };
+        if constexpr (STREAM) {
+          for (int c = nch - 1; c >= 0; --c) {
+            double la[MAXL], lb[MAXL];
+            build_chunk(c, la, lb);
+            scan(la, lb, c * 64 * MAXL);
+          }
+        } else {
+          double la[MAXL], lb[MAXL];
+          build_lines(la, lb);
+          scan(la, lb, 0);
+        }
+        DKG_BUTTERFLY({
+          const int st = S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32;
+          kL = min(kL, __shfl_xor(kL, st));
+          kT = min(kT, __shfl_xor(kT, st));
+          kR = min(kR, __shfl_xor(kR, st));
+        })
+        f.kL = __builtin_amdgcn_readfirstlane(kL);
+        f.kT = __builtin_amdgcn_readfirstlane(kT);
+        f.kR = __builtin_amdgcn_readfirstlane(kR);
+        f.cntT = ct;
+      }
+      auto known = [&](double, double) -> int { return -1; };  // every vertex index is known now
       if (f.status == 1) {
         kgj = 0.0;
       } else {
         if (f.status == 0) {
-          kgj = envelope_hull_visit(f, lane, sb, sa, si, visit);
+          kgj = envelope_hull_visit(f, lane, sb, sa, si, visit, known);
         } else if constexpr (STREAM) {
-          kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, visit);
+          kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, visit, f.kL);
         } else {
           double la[MAXL], lb[MAXL];
           build_lines(la, lb);
-          kgj = envelope_walk_visit<MAXL>(la, lb, NL, lane, f, visit);
+          kgj = envelope_walk_visit<MAXL>(la, lb, NL, lane, f, visit, [&](double, double) { return f.kL; });
         }
         // - sum_e Dw_e b_e * dV/(2V), - [line 0 attains max a] da_0/dx
         double a0 = a_off;
@@ -998,27 +994,15 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     } else {
       double la[MAXL], lb[MAXL];
       build_lines(la, lb);
-      if (dbg & 1) {  // ablation: lines + one reduction only
-        double mxv = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < MAXL; ++t) mxv = fmax(mxv, la[t] + lb[t]);
-        f.status = 3;
-        f.aT = wave_max(mxv);
-      } else {
-        f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
-      }
+      f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
     }
     if constexpr (GRAD) {
-    } else if (f.status == 3) {
-      kgj = f.aT;
     } else if (f.status == 1) {
       kgj = 0.0;
-    } else if (dbg & 32) {  // debug: report the candidate count instead of KG
-      kgj = (double)(f.cnt + 3);
     } else if (f.status == 0) {
-      kgj = envelope_hull(f, lane, sb, sa, nullptr, dbg);
+      kgj = envelope_hull(f, lane, sb, sa, nullptr);
     } else if constexpr (STREAM) {  // list overflow: gift wrap over the streamed lines
-      kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, noop_visit);
+      kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, noop_visit, -1);
     } else {  // list overflow: gift wrap over the (rebuilt) register lines
       double la[MAXL], lb[MAXL];
       build_lines(la, lb);
@@ -1047,7 +1031,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     const int G = gridDim.y;
     if (G == 1) {
       kg[b] = s / (double)S;
-    } else if (G == 2 || (dbg & 2)) {
+    } else if (G == 2) {
       // two addends onto a zeroed cell: fp addition commutes, so the order
       // the two workgroups arrive in does not change the bits.
       atomicAdd(&kg[b], s / (double)S);

@@ -294,7 +294,6 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   const int oi = blockIdx.z;
   const dkg_output& o = P->o[oi];
   const int N = P->N;
-  const int dbg = P->debug_cov;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tt = wave & 3, half = wave >> 2;
@@ -337,10 +336,6 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
         va[u] = frag_pair(P->q[oi], ti, j, lane, KB);
         vd[u] = frag_pair(dsrc, dt, j, lane, KB);
       }
-      if (dbg & 1) {
-#pragma unroll
-        for (int u = 0; u < PC_P; ++u) { va[u] = double2{1.0, 1.0}; vd[u] = double2{0.5, 0.5}; }
-      }
 #pragma unroll
       for (int u = 0; u < PC_P; ++u) {
         const bool in = pb + u < p1 && have_d;
@@ -372,7 +367,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
       const int b = ti * 16 + (lane >> 4) + 4 * r;
       if (b < B && k < N)
         P->cov[oi][(size_t)b * N + k] =
-            ((dbg & 4) ? r2[r] : o.outputscale * kernel_profile(o.kernel, r2[r])) - sum;
+            o.outputscale * kernel_profile(o.kernel, r2[r]) - sum;
     }
     if (want_var && lane < 16) {
       const int bb = ti * 16 + lane;
