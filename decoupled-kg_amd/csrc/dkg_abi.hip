@@ -35,6 +35,8 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct WsLayout {
   size_t jq[DKG_MAX_OUTPUTS];
   size_t gmu[DKG_MAX_OUTPUTS];
+  size_t qxrm[DKG_MAX_OUTPUTS];
+  size_t qdrm[DKG_MAX_OUTPUTS];
   size_t q[DKG_MAX_OUTPUTS];
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
@@ -55,6 +57,10 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
       off = align256(off + (size_t)d * Bp * pad16(outs[i].n) * sizeof(double));
       L.gmu[i] = off;
       off = align256(off + (size_t)d * Bp * sizeof(double));
+      L.qxrm[i] = off;
+      off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
+      L.qdrm[i] = off;
+      off = align256(off + (size_t)std::max(N, 1) * pad16(outs[i].n) * sizeof(double));
     }
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
@@ -125,7 +131,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
-  if (flags & ~DKG_PLAN_GRAD) return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
+  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK)) return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
   if (want_grad && envelope_grad_lds_bytes(m, N, sw, S, d, max_np, true) > 160 * 1024)
     return fail(DKG_ERR_UNSUPPORTED, "gradient: m=%d outputs, n=%d, d=%d exceed the envelope stage's LDS", m, max_np,
                 d);
@@ -154,6 +160,8 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
     if (P->grad) {
       P->jq[i] = reinterpret_cast<double*>(ws + L.jq[i]);
       P->gmu[i] = reinterpret_cast<double*>(ws + L.gmu[i]);
+      P->qxrm[i] = reinterpret_cast<double*>(ws + L.qxrm[i]);
+      P->qdrm[i] = reinterpret_cast<double*>(ws + L.qdrm[i]);
     }
     P->q[i] = reinterpret_cast<double*>(ws + L.q[i]);
     P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
@@ -169,7 +177,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
   static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
   static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
-  P->debug_env = denv ? std::atoi(denv) : 0;
+  P->debug_env = (denv ? std::atoi(denv) : 0) | ((flags & DKG_PLAN_FORCE_WALK) ? 1 : 0);
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
   static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
   P->debug_stamp = dst ? std::atoi(dst) : 0;
@@ -208,9 +216,12 @@ size_t plan_slot_bytes() { return align256(sizeof(Plan)); }
 // mu_D of every output into the plan's contiguous [m][N] block (stream ordered).
 int copy_disc_means(const Plan& P, hipStream_t s) {
   for (int i = 0; i < P.m && P.N > 0; ++i) {
-    const int st = hip_check(hipMemcpyAsync(P.mu_all + (size_t)i * P.N, P.o[i].disc_mean, sizeof(double) * P.N,
-                                            hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(mu_D)");
+    int st = hip_check(hipMemcpyAsync(P.mu_all + (size_t)i * P.N, P.o[i].disc_mean, sizeof(double) * P.N,
+                                      hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(mu_D)");
     if (st) return st;
+    // GRAD: row-major Q_D for the envelope's per-line row gathers
+    if (P.grad && (st = hip_check(launch_unpack_rows(P.o[i].disc_frag, P.N, P.o[i].n, P.qdrm[i], s), "unpack_rows")))
+      return st;
   }
   return DKG_OK;
 }

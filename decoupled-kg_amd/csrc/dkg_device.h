@@ -62,6 +62,7 @@ __device__ __forceinline__ unsigned long long* kst_slot(int dst, const Plan* P, 
 // multiplication); the hull edges are collected one per lane and psi is
 // evaluated for all of them at once.
 constexpr int ENV_CAP = 128;
+constexpr int HCAP = 128;  // GRAD: queued envelope lines per wave before their gradient terms are flushed
 constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lines)  // survivor list per wave (overflow -> walk all lines)
 
 // Gift wrap over all register lines (fallback when the survivor list
@@ -184,7 +185,11 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
     const double a = la[t], bb = lb[t];
-    const bool s = fma(a, db1, -bb * da1) > k1 || fma(a, db2, -bb * da2) > k2;
+    bool s = fma(a, db1, -bb * da1) > k1 || fma(a, db2, -bb * da2) > k2;
+    // IDX: also every exact copy of L and R and every line attaining max a, so
+    // the list carries their indices (lowest index among duplicates) and the
+    // max-a count without another pass over the lines
+    if constexpr (IDX) s = s || a == aT || (bb == bL && a == aL) || (bb == bR && a == aR);
     const uint64_t mk = __ballot(s);
     if (mk != 0) {  // wave-uniform, rarely taken
       if (s) {
@@ -200,7 +205,7 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
   }
   f.cnt = cnt;
   f.status = (cnt + 3 > ENV_CAP) ? 2 : 0;
-  // IDX: the line indices of L, T, R and the count of max-a lines are
+  // IDX (list overflow only): the line indices of L, T, R and the count of max-a lines are
   // resolved lazily by the caller (rarely needed; keeps register pressure low)
   f.kL = f.kT = f.kR = -1;
   f.cntT = -1;
@@ -292,32 +297,58 @@ __device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, do
 // each with its breakpoints (cL, cR) (-inf / +inf at the ends), passed to
 // visit(k, b, a, cL, cR); the return value is KG_w as in the forward.
 
-// From the candidate list of an IDX filter (si holds the line indices).
-template <class Visit, class Resolve>
-__device__ __forceinline__ double envelope_hull_visit(const EnvFilter& f, int lane, double* sb, double* sa, int* si,
-                                                      Visit&& visit, Resolve&& resolve) {
-  const int cnt = f.cnt;
-  const double bT = f.bT;
-  if (lane == 0) {
-    sb[cnt] = f.bL; sa[cnt] = f.aL; si[cnt] = f.kL;
-    sb[cnt + 1] = f.bT; sa[cnt + 1] = f.aT; si[cnt + 1] = f.kT;
-    sb[cnt + 2] = f.bR; sa[cnt + 2] = f.aR; si[cnt + 2] = f.kR;
-  }
-  const int nc = cnt + 3;
+// Gradient hull over the candidate list of an IDX filter (every entry's line
+// index known, exact copies of L / R and all max-a lines included).  The
+// chain from L is followed serially (one v_readlane per vertex); everything
+// else is vertex-parallel, one hull vertex per lane: breakpoints cL / cR,
+// dE/da = Phi(cR) - Phi(cL), dE/db = phi(cL) - phi(cR), the KG edge terms and
+// the queue of envelope lines k >= 1 (index, dE/db) for the gradient flush.
+struct HullGrad {
+  double kg;     // KG_w (same edge sum as envelope_hull)
+  double sumDb;  // sum over hull lines of dE/db * b
+  double Pw0, Dw0;  // line 0 (the candidate itself) if on the hull, else 0
+  int nq;        // queued lines k >= 1 (hk / hD)
+  int cntT;      // lines attaining max a
+};
+
+__device__ __forceinline__ HullGrad envelope_hull_grad(const EnvFilter& f, int lane, const double* sb,
+                                                       const double* sa, const int* si, double* scl, int* hk,
+                                                       double* hD, int N) {
+  HullGrad r;
+  const int nc = f.cnt;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   double lb_[2], la_[2];
   int li_[2];
+  bool ok[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int e = min(c * 64 + lane, nc - 1);
+    ok[c] = c * 64 + lane < nc;
     lb_[c] = sb[e];
     la_[c] = sa[e];
     li_[c] = si[e];
   }
+  // chain start: the lowest-index copy of L; and the max-a count
+  int kst = 1 << 30, cntT = 0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (ok[c] && lb_[c] == f.bL && la_[c] == f.aL) kst = min(kst, li_[c]);
+    cntT += __popcll(__ballot(ok[c] && la_[c] == f.aT));
+  }
+  DKG_BUTTERFLY({
+    const int o = __shfl_xor(kst, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
+    kst = min(kst, o);
+  })
+  int start;
+  {
+    const uint64_t m0 = __ballot(ok[0] && li_[0] == kst), m1 = __ballot(ok[1] && li_[1] == kst);
+    start = m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1);
+  }
+  // right neighbour of every entry (as envelope_hull)
   int nxt[2] = {-1, -1};
-  double cn[2] = {0.0, 0.0}, cd[2] = {1.0, 1.0};
+  double cn[2] = {0.0, 0.0}, cd[2] = {1.0, 1.0}, cb[2] = {0.0, 0.0};
   const int nc0 = min(nc, 64);
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -337,80 +368,59 @@ __device__ __forceinline__ double envelope_hull_visit(const EnvFilter& f, int la
 #pragma unroll 4
     for (int j = 0; j < nc0; ++j) consider(readlane_f64(lb_[0], j), readlane_f64(la_[0], j), j);
     for (int j = 64; j < nc; ++j) consider(readlane_f64(lb_[1], j - 64), readlane_f64(la_[1], j - 64), j);
-    nxt[c] = rj; cn[c] = rn; cd[c] = rd;
+    nxt[c] = rj; cn[c] = rn; cd[c] = rd; cb[c] = rb;
   }
-  // chain from L (index cnt) to R, one vertex per step
-  double kg = 0.0, cL = -INFINITY;
-  int cur = cnt;
-  for (int guard = 0; guard < nc; ++guard) {
-    const bool hi = cur >= 64;
-    const int ln = cur & 63;
-    const double bP = readlane_f64(hi ? lb_[1] : lb_[0], ln);
-    const double aP = readlane_f64(hi ? la_[1] : la_[0], ln);
-    int kP = __builtin_amdgcn_readlane(hi ? li_[1] : li_[0], ln);
-    if (kP < 0) kP = resolve(bP, aP);  // L, T or R: find its line index
-    const int nx = __builtin_amdgcn_readlane(hi ? nxt[1] : nxt[0], ln);
-    double cR = INFINITY;
-    if (nx >= 0) {
-      cR = readlane_f64(hi ? cn[1] : cn[0], ln) / readlane_f64(hi ? cd[1] : cd[0], ln);
-      const double bQ = readlane_f64(nx >= 64 ? lb_[1] : lb_[0], nx & 63);
-      kg += (bQ - bP) * psi((bQ <= bT) ? -cR : cR);
-    }
-    visit(kP, bP, aP, cL, cR);
-    if (nx < 0) break;
-    cL = cR;
-    cur = nx;
+  // follow the chain from the start: its members are the envelope lines
+  uint64_t on0 = 0, on1 = 0;
+  for (int cur = start, guard = 0; cur >= 0 && guard < nc; ++guard) {
+    if (cur < 64) on0 |= 1ull << cur; else on1 |= 1ull << (cur - 64);
+    cur = (cur < 64) ? __builtin_amdgcn_readlane(nxt[0], cur) : __builtin_amdgcn_readlane(nxt[1], cur - 64);
   }
-  return kg;
-}
-
-// Gift wrap over register lines with the line index carried (list overflow).
-template <int MAXL, class Visit, class Resolve>
-__device__ __forceinline__ double envelope_walk_visit(const double (&la)[MAXL], const double (&lb)[MAXL], int nl,
-                                                      int lane, const EnvFilter& f, Visit&& visit,
-                                                      Resolve&& resolve) {
-  double bc = f.bL, ac = f.aL, kg = 0.0, cL = -INFINITY;
-  int kc = resolve(f.bL, f.aL);
-  for (int guard = 0; guard <= nl; ++guard) {
-    if (!uniform(bc < f.bR)) break;
-    double bn = INFINITY, bd = 1.0, bbest = -INFINITY, abest = -INFINITY;
-    int kbest = 1 << 30;
+  // left breakpoints: every hull vertex hands its right breakpoint to its successor
+  double cR[2];
+  bool on[2];
 #pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      const double bb = lb[t], a = la[t];
-      if (lane + 64 * t < nl && bb > bc) {
-        const double num = ac - a, den = bb - bc;
-        const double lhs = num * bd, rhs = bn * den;
-        if (bbest == -INFINITY || lhs < rhs || (lhs == rhs && (bb > bbest || (bb == bbest && a > abest)))) {
-          bn = num; bd = den; bbest = bb; abest = a; kbest = lane + 64 * t;
-        }
-      }
-    }
-    DKG_BUTTERFLY({
-      const double on = partner_f64<S_>(bn), od = partner_f64<S_>(bd);
-      const double ob = partner_f64<S_>(bbest), oa = partner_f64<S_>(abest);
-      const int ok = __shfl_xor(kbest, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
-      bool take;
-      if (ob == -INFINITY) take = false;
-      else if (bbest == -INFINITY) take = true;
-      else {
-        const double lhs = on * bd, rhs = bn * od;
-        take = lhs < rhs ||
-               (lhs == rhs && (ob > bbest || (ob == bbest && (oa > abest || (oa == abest && ok < kbest)))));
-      }
-      if (take) { bn = on; bd = od; bbest = ob; abest = oa; kbest = ok; }
-    })
-    if (!uniform(bbest > bc)) break;
-    const double c = bn / bd;
-    kg += (bbest - bc) * psi((bbest <= f.bT) ? -c : c);
-    visit(kc, bc, ac, cL, c);
-    cL = c;
-    bc = bbest;
-    ac = abest;
-    kc = __builtin_amdgcn_readfirstlane(kbest);
+  for (int c = 0; c < 2; ++c) {
+    on[c] = (((c == 0) ? on0 : on1) >> lane) & 1;
+    cR[c] = (nxt[c] >= 0) ? cn[c] / cd[c] : INFINITY;
   }
-  visit(kc, bc, ac, cL, INFINITY);
-  return kg;
+  if (lane == 0) scl[start] = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+    if (on[c] && nxt[c] >= 0) scl[nxt[c]] = cR[c];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double kg = 0.0, sdb = 0.0, pw0 = 0.0, dw0 = 0.0;
+  int nq = 0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c * 64 >= nc) break;
+    double Dw = 0.0;
+    if (on[c]) {
+      const double cl = scl[c * 64 + lane], cr = cR[c];
+      if (nxt[c] >= 0) kg += (cb[c] - lb_[c]) * psi((cb[c] <= f.bT) ? -cr : cr);
+      const double Pw = norm_cdf(cr) - norm_cdf(cl);
+      Dw = norm_pdf(cl) - norm_pdf(cr);
+      sdb = fma(Dw, lb_[c], sdb);
+      if (li_[c] == 0) { pw0 = Pw; dw0 = Dw; }
+    }
+    const bool q = on[c] && li_[c] >= 1 && li_[c] <= N;
+    const uint64_t mq = __ballot(q);
+    if (q) {
+      const int pos = nq + lanes_below(mq);
+      hk[pos] = li_[c];
+      hD[pos] = Dw;
+    }
+    nq += __popcll(mq);
+  }
+  r.kg = wave_sum(kg);
+  r.sumDb = wave_sum(sdb);
+  r.Pw0 = wave_sum(pw0);  // at most one lane holds line 0
+  r.Dw0 = wave_sum(dw0);
+  r.nq = nq;
+  r.cntT = cntT;
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -469,7 +479,8 @@ __device__ __forceinline__ EnvFilter envelope_filter_stream(int nch, int lane, d
 #pragma unroll
     for (int t = 0; t < MAXL; ++t) {
       const double a = la[t], bb = lb[t];
-      const bool s = fma(a, db1, -bb * da1) > k1 || fma(a, db2, -bb * da2) > k2;
+      bool s = fma(a, db1, -bb * da1) > k1 || fma(a, db2, -bb * da2) > k2;
+      if constexpr (IDX) s = s || a == aT || (bb == bL && a == aL) || (bb == bR && a == aR);
       const uint64_t mk = __ballot(s);
       if (mk != 0) {
         if (s) {
@@ -596,6 +607,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   __shared__ double s_tail[16];
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space)
   __shared__ double s_pp[DKG_MAX_OUTPUTS * 6];
+  __shared__ int s_kind[DKG_MAX_OUTPUTS];  // GRAD: covariance family per output
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   const int g = blockIdx.y;
@@ -634,8 +646,13 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   // candidate's q_i and J_i rows, gv / gm / per-wave gradient scratch, x_b.
   const int d = P->d;
   const int NP = P->max_np;
+  const double* disc = GRAD ? P->disc : nullptr;
+  // test hook (DKG_PLAN_FORCE_WALK): every pair takes the list-overflow path
+  const bool force_walk = __builtin_amdgcn_readfirstlane(P->debug_env) & 1;
   int* sidx = nullptr;
   double *qrow = nullptr, *jrow = nullptr, *sgv = nullptr, *sgm = nullptr, *sgw = nullptr, *sx = nullptr;
+  double *sil = nullptr, *shD = nullptr, *suw = nullptr, *sscl = nullptr;
+  int* shk = nullptr;
   if constexpr (GRAD) {
     double* gb = sbuf + (size_t)SW * 2 * ENV_CAP;
     sidx = reinterpret_cast<int*>(gb);
@@ -645,6 +662,11 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     sgm = sgv + M * DKG_MAX_DIM;                     // [M][16]  d mu_i / dx
     sgw = sgm + M * DKG_MAX_DIM;                     // [SW][64] per wave: gacc | ga0 | gvv | gtot
     sx = sgw + SW * 64;                              // [16]     x_b
+    sil = sx + DKG_MAX_DIM;                          // [M][16]  1 / lengthscale per output
+    shD = sil + M * DKG_MAX_DIM;                     // [SW][HCAP] per wave: pending hull lines' dE/db
+    suw = shD + SW * HCAP;                           // [SW][NP]   per wave: u_i = sum_h coef_h Q_D,i[k_h]
+    sscl = suw + (size_t)SW * NP;                    // [SW][ENV_CAP] per wave: left breakpoints of hull vertices
+    shk = reinterpret_cast<int*>(sscl + SW * ENV_CAP);  // [SW][HCAP] pending hull lines' indices
   }
 
   // ---- one round of memory traffic: DMA the line data, plain loads for the rest
@@ -659,6 +681,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     pp[3] = o->outputscale;
     pp[4] = var_all[(size_t)threadIdx.x * bpad + b];
     pp[5] = mux_all[(size_t)threadIdx.x * bpad + b];
+    if constexpr (GRAD) s_kind[threadIdx.x] = o->kernel;
   }
   const double* wsrc = wts;
 #pragma unroll
@@ -678,12 +701,13 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       if (i < m) {
-        const int npi = pad16(P->o[i].n), KBi = npi / 4;
+        const int npi = pad16(P->o[i].n);
         const size_t mat = (size_t)P->bpad * npi;
+        const double* qx = P->qxrm[i] + (size_t)b * npi;
+        const double* jq = P->jq[i] + (size_t)b * npi;
         for (int c = threadIdx.x; c < NP; c += blockDim.x) {
-          const size_t fi = frag_index(b >> 4, c >> 2, ((c & 3) << 4) | (b & 15), KBi);
-          qrow[(size_t)i * NP + c] = (c < npi) ? P->q[i][fi] : 0.0;
-          for (int dd = 0; dd < d; ++dd) jrow[((size_t)i * d + dd) * NP + c] = (c < npi) ? P->jq[i][dd * mat + fi] : 0.0;
+          qrow[(size_t)i * NP + c] = (c < npi) ? qx[c] : 0.0;
+          for (int dd = 0; dd < d; ++dd) jrow[((size_t)i * d + dd) * NP + c] = (c < npi) ? jq[dd * mat + c] : 0.0;
         }
       }
     }
@@ -692,11 +716,15 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       sgm[i * DKG_MAX_DIM + dd] = P->gmu[i][(size_t)dd * P->bpad + b];
     }
     if (threadIdx.x < d) sx[threadIdx.x] = xnew[(size_t)b * d + threadIdx.x];
+    if (threadIdx.x < m * d) {
+      const int i = threadIdx.x / d, dd = threadIdx.x % d;
+      sil[i * DKG_MAX_DIM + dd] = P->o[i].inv_lengthscale[dd];
+    }
   }
-  KST(st, 2);
+  if (!GRAD) KST(st, 2);  // GRAD stamps: 2 preamble done, 3 filter, 4 hull, 5 gradient flush (first pair)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  KST(st, 3);
+  if (!GRAD) KST(st, 3);
 
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
   double* sa = sb + ENV_CAP;
@@ -716,6 +744,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     }
     gw[lane] = 0.0;
     __syncthreads();
+    KST(st, 2);
   }
   const int waves_total = SW * gridDim.y;
   double sv[M], mx0[M], ysd[M], ymu[M], nz[M], os[M];
@@ -861,6 +890,8 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
         build_lines(la, lb);
         f = envelope_filter<MAXL, true>(la, lb, lane, sb, sa, si);
       }
+      if (force_walk && f.status == 0) f.status = 2;
+      if (j == g * SW + wave) KST(st, 3);
       double Vden = den;  // the variance under the square root of the slopes
       if (!full) {
         const double sd2 = ysd[target] * ysd[target];
@@ -882,9 +913,128 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
         }
       }
       double sumDb = 0.0;
+      // Envelope lines k >= 1 are queued (index, dE/db) in the wave's list and
+      // their gradient terms evaluated together by flush(): the kernel
+      // derivative one line per lane, and J_i^T Q_D,i[k] as one dot per
+      // (output, coordinate) against u_i = sum_h coef_h Q_D,i[k_h], so the
+      // gathers of all queued rows are independent and the wave sums are paid
+      // once per flush instead of once per line.
+      int* hk = shk + wave * HCAP;
+      double* scl = sscl + wave * ENV_CAP;
+      double* hD = shD + wave * HCAP;
+      double* uw = suw + (size_t)wave * NP;
+      int nh = 0;
+      auto flush = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // kernel-derivative terms: lane h handles queued line h
+        {
+          const bool act = lane < nh;
+          const int k = act ? hk[lane] : 1;
+          const double Dw = act ? hD[lane] : 0.0;
+          const double* z = disc + (size_t)(k - 1) * d;
+          double hc[M];
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            hc[i] = 0.0;
+            if (i < m && wb[i] != 0.0) {
+              double r2 = 0.0;
+              for (int dd = 0; dd < d; ++dd) {
+                const double t = (sx[dd] - z[dd]) * sil[i * DKG_MAX_DIM + dd];
+                r2 = fma(t, t, r2);
+              }
+              hc[i] = Dw * wb[i] * os[i] * kernel_dprofile(__builtin_amdgcn_readfirstlane(s_kind[i]), r2);
+            }
+          }
+          for (int dd = 0; dd < d; ++dd) {
+            const double t = sx[dd] - z[dd];
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+              const double il = sil[((i < m) ? i : 0) * DKG_MAX_DIM + dd];
+              v = fma(hc[i] * t, il * il, v);
+            }
+            v = wave_sum(v);
+            if (lane == 0) gw[dd] += v;
+          }
+        }
+        // - sum_h coef_h J_i^T Q_D,i[k_h - 1]
+        if (uniform(NP <= 256)) {
+          // every output's rows of every queued line in flight together; the
+          // dots J_i^T u_i come straight from the registers
+          double u[M][4];
+          const double* qd[M];
+          int npo[M];
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            qd[i] = P->qdrm[(i < m) ? i : 0];
+            npo[i] = pad16(P->o[(i < m) ? i : 0].n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) u[i][q] = 0.0;
+          }
+#pragma unroll 4
+          for (int h = 0; h < nh; ++h) {
+            const int r = hk[h] - 1;
+            const double dw = hD[h];
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+              if (i < m) {
+                const double* row = qd[i] + (size_t)r * npo[i];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) u[i][q] = fma(dw, row[min(lane + 64 * q, npo[i] - 1)], u[i][q]);
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            if (i < m && wb[i] != 0.0) {
+              for (int dd = 0; dd < d; ++dd) {
+                const double* jr = jrow + ((size_t)i * d + dd) * NP;
+                double acc = 0.0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (lane + 64 * q < npo[i]) acc = fma(jr[lane + 64 * q], u[i][q], acc);
+                acc = wave_sum(acc);
+                if (lane == 0) gw[dd] -= acc * wb[i];
+              }
+            }
+          }
+        } else {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          if (i < m && wb[i] != 0.0) {
+            const double* qd = P->qdrm[i];
+            const int npi = pad16(P->o[i].n);
+            for (int c0 = 0; c0 < npi; c0 += 4 * 64) {
+              // 4 column chunks of every queued row in flight together
+              double u[4] = {0.0, 0.0, 0.0, 0.0};
+              const int c = c0 + lane;
+              for (int h = 0; h < nh; ++h) {
+                const double* row = qd + (size_t)(hk[h] - 1) * npi;
+                const double dw = hD[h];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) u[q] = fma(dw, row[min(c + 64 * q, npi - 1)], u[q]);
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (c + 64 * q < npi) uw[c + 64 * q] = u[q] * wb[i];
+            }
+            for (int dd = 0; dd < d; ++dd) {
+              const double* jr = jrow + ((size_t)i * d + dd) * NP;
+              double acc = 0.0;
+              for (int c = lane; c < npi; c += 64) acc = fma(jr[c], uw[c], acc);
+              acc = wave_sum(acc);
+              if (lane == 0) gw[dd] -= acc;
+            }
+          }
+        }
+        }
+        nh = 0;
+      };
       // one envelope line: d/dx of its slope (and of line 0's intercept), weighted
       // by dE/db = phi(cL) - phi(cR) and dE/da = Phi(cR) - Phi(cL)
-      auto visit = [&](int k, double bP, double aP, double cL, double cR) {
+      auto visit = [&](int k, double bP, double aP, double cL, double cR) __attribute__((always_inline)) {
         (void)aP;
         const double Pw = norm_cdf(cR) - norm_cdf(cL);
         const double Dw = norm_pdf(cL) - norm_pdf(cR);
@@ -900,39 +1050,17 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
             }
           }
         } else if (k <= N) {
-          const double* z = P->disc + (size_t)(k - 1) * d;
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            if (i < m && wb[i] != 0.0) {
-              const dkg_output& o = P->o[i];
-              double r2 = 0.0;
-              for (int dd = 0; dd < d; ++dd) {
-                const double t = (sx[dd] - z[dd]) * o.inv_lengthscale[dd];
-                r2 = fma(t, t, r2);
-              }
-              const double coef = Dw * wb[i];
-              const double hc = coef * os[i] * kernel_dprofile(o.kernel, r2);
-              // J_i^T Q_D,i[k-1]: lanes over the training columns, one coordinate at a time
-              const int npi = pad16(o.n), KBi = npi / 4, r = k - 1;
-              for (int dd = 0; dd < d; ++dd) {
-                double acc = 0.0;
-                for (int c = lane; c < npi; c += 64)
-                  acc = fma(jrow[((size_t)i * d + dd) * NP + c],
-                            o.disc_frag[frag_index(r >> 4, c >> 2, ((c & 3) << 4) | (r & 15), KBi)], acc);
-                acc = wave_sum(acc);
-                if (lane == 0) {
-                  const double il = o.inv_lengthscale[dd];
-                  gw[dd] += hc * (sx[dd] - z[dd]) * il * il - coef * acc;
-                }
-              }
-            }
+          if (lane == 0) {
+            hk[nh] = k;
+            hD[nh] = Dw;
           }
+          if (++nh == HCAP) flush();
         }
       };
       // line indices of L, T, R (lowest among exact duplicates) and the number
       // of lines attaining max a: one pass over the rebuilt lines, after the
       // filter has released its registers
-      if (f.status != 1) {
+      if (f.status == 2) {
         int kL = 1 << 30, kT = 1 << 30, kR = 1 << 30, ct = 0;
         auto scan = [&](const double (&la)[MAXL], const double (&lb)[MAXL], int base) {
 #pragma unroll
@@ -966,19 +1094,35 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
         f.kR = __builtin_amdgcn_readfirstlane(kR);
         f.cntT = ct;
       }
-      auto known = [&](double, double) -> int { return -1; };  // every vertex index is known now
       if (f.status == 1) {
         kgj = 0.0;
       } else {
         if (f.status == 0) {
-          kgj = envelope_hull_visit(f, lane, sb, sa, si, visit, known);
+          const HullGrad hg = envelope_hull_grad(f, lane, sb, sa, si, scl, hk, hD, N);
+          kgj = hg.kg;
+          sumDb = hg.sumDb;
+          nh = hg.nq;
+          f.cntT = hg.cntT;
+          if (lane == 0) {  // line 0 (the candidate): d b_0 and d a_0 terms
+            for (int dd = 0; dd < d; ++dd) {
+              double gvs = 0.0;
+#pragma unroll
+              for (int i = 0; i < M; ++i)
+                if (i < m) gvs = fma(wb[i], sgv[i * DKG_MAX_DIM + dd], gvs);
+              gw[dd] += hg.Dw0 * gvs + hg.Pw0 * gw[16 + dd];
+            }
+          }
         } else if constexpr (STREAM) {
           kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, visit, f.kL);
         } else {
-          double la[MAXL], lb[MAXL];
-          build_lines(la, lb);
-          kgj = envelope_walk_visit<MAXL>(la, lb, NL, lane, f, visit, [&](double, double) { return f.kL; });
+          // list overflow: gift wrap, rebuilding the staged lines every step so
+          // no register lines stay live across the visits
+          auto rebuild = [&](int, double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
+          kgj = envelope_walk_stream<MAXL>(1, NL, lane, f, rebuild, visit, f.kL);
         }
+        if (j == g * SW + wave) KST(st, 4);
+        if (nh > 0) flush();
+        if (j == g * SW + wave) KST(st, 5);
         // - sum_e Dw_e b_e * dV/(2V), - [line 0 attains max a] da_0/dx
         double a0 = a_off;
 #pragma unroll
@@ -991,10 +1135,12 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
         for (int dd = 0; dd < d; ++dd) gw[dd] = 0.0;
     } else if constexpr (STREAM) {
       f = envelope_filter_stream<MAXL, false>(nch, lane, sb, sa, nullptr, build_chunk);
+      if (force_walk && f.status == 0) f.status = 2;
     } else {
       double la[MAXL], lb[MAXL];
       build_lines(la, lb);
       f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
+      if (force_walk && f.status == 0) f.status = 2;
     }
     if constexpr (GRAD) {
     } else if (f.status == 1) {
@@ -1013,10 +1159,10 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
 
   // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
-  KST(st, 4);
+  if (!GRAD) KST(st, 4);
   if (lane == 0) s_tail[wave] = wave_acc;
   __syncthreads();
-  KST(st, 5);
+  if (!GRAD) KST(st, 5);
   if constexpr (GRAD) {
     if (threadIdx.x < d) {
       double gs = 0.0;

@@ -26,7 +26,9 @@ struct Plan {
   double* mux[DKG_MAX_OUTPUTS];     // posterior mean at the candidates per output (workspace)
   double* var[DKG_MAX_OUTPUTS];     // noiseless posterior variance s - |Q_X[b]|^2 per output (workspace)
   double* cov[DKG_MAX_OUTPUTS];     // [B x N] posterior covariance rows per output (workspace)
-  double* jq[DKG_MAX_OUTPUTS];      // GRAD: d fragment-packed dK(x,X)/dx_g R matrices (bpad x n_pad each)
+  double* jq[DKG_MAX_OUTPUTS];      // GRAD: J_g = dK(x,X)/dx_g R, row-major [d][bpad][n_pad] per output
+  double* qxrm[DKG_MAX_OUTPUTS];    // GRAD: Q_X = K(x,X) R row-major [bpad][n_pad] per output
+  double* qdrm[DKG_MAX_OUTPUTS];    // GRAD: Q_D = K(D,X) R row-major [N][n_pad] per output (written at plan init)
   double* gmu[DKG_MAX_OUTPUTS];     // GRAD: [d][bpad] model-space mean gradients
   unsigned long long* kstamps;      // debug_stamp: [3][KST_WG][8] phase stamps (device)
   double* mux_all;                  // [m][bpad]  = mux[0..m)
@@ -50,6 +52,8 @@ struct CrossArgs {
 hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, int n1, const double* x2, int n2,
                                 double diag_add, double* out, hipStream_t s);
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
+// Row-major copy [rows][n_pad] of a fragment-packed (rows x n) matrix.
+hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
 // Value and gradient: kg[B] and dkg[B x d] (d KG(x_b) / d x_b), plan built with DKG_PLAN_GRAD.
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,

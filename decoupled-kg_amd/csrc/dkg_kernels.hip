@@ -40,6 +40,17 @@ __global__ void pack_root_kernel(const double* __restrict__ r, int n, double* __
   }
 }
 
+// out[r][c] (row-major, n_pad columns) = element (r, c) of a fragment-packed
+// (rows x n) matrix; one thread per output element, coalesced stores.
+__global__ void unpack_rows_kernel(const double* __restrict__ frag, int rows, int np, double* __restrict__ out) {
+  const int KB = np / 4;
+  const size_t total = (size_t)rows * np;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / np), c = (int)(e % np);
+    out[e] = frag[frag_index(r >> 4, c >> 2, ((c & 3) << 4) | (r & 15), KB)];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // cross_root_kernel: one workgroup per (16-row tile ti, tile pair p, output).
 // The pair is (p, T-1-p) of 16-column tiles of Q = K_x R; R upper triangular
@@ -57,7 +68,9 @@ constexpr int CR_U = 8;  // k-blocks per load batch
 template <int DM, bool GRAD = false>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
                                                 double* __restrict__ qout, double* __restrict__ mout, int ti, int p,
-                                                double* smem, unsigned long long* st = nullptr, int gdim = 0) {
+                                                double* smem, unsigned long long* st = nullptr, int gdim = 0,
+                                                const double* __restrict__ qx_frag = nullptr,
+                                                double* __restrict__ qx_rm = nullptr) {
   const int n = o.n;
   const int np = pad16(n);
   const int T = np / 16;
@@ -210,7 +223,15 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       for (int w = 0; w < CR_WAVES; ++w) s += part[(w * 8 + tsel * 4 + r) * 64 + lane];
       const int tj = tsel ? tB : tA;
       // D = R^T K^T: lane holds Q[16ti + (l&15)][16tj + 4r + (l>>4)] = q_frag[ti][4tj + r][l]
-      qout[frag_index(ti, 4 * tj + r, lane, KB)] = s;
+      if constexpr (GRAD) {
+        // J row-major [bpad][np] for the envelope's per-candidate row loads;
+        // the gdim == 0 workgroups also copy Q_X's matching entries row-major
+        const size_t rm = (size_t)(16 * ti + (lane & 15)) * np + 16 * tj + 4 * r + (lane >> 4);
+        qout[rm] = s;
+        if (qx_rm) qx_rm[rm] = qx_frag[frag_index(ti, 4 * tj + r, lane, KB)];
+      } else {
+        qout[frag_index(ti, 4 * tj + r, lane, KB)] = s;
+      }
     }
   }
   if (want_mean && tid < 16) {
@@ -264,7 +285,7 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_grad_plan_kernel(const 
   const dkg_output& o = P->o[oi];
   const size_t mat = (size_t)P->bpad * pad16(o.n);
   cross_root_impl<DM, true>(o, d, xnew, B, P->jq[oi] + gdim * mat, P->gmu[oi] + (size_t)gdim * P->bpad, blockIdx.x,
-                            blockIdx.y, smem, st, gdim);
+                            blockIdx.y, smem, st, gdim, P->q[oi], gdim == 0 ? P->qxrm[oi] : nullptr);
 }
 
 size_t cross_root_lds_bytes(int np, int d) {
@@ -388,7 +409,9 @@ size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream) {
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream) {
   const int M = outputs_bucket(m);
   const size_t extra = (size_t)(waves * ENV_CAP + 1) / 2 + (size_t)M * max_np + (size_t)M * d * max_np +
-                       2 * (size_t)M * DKG_MAX_DIM + (size_t)waves * 64 + DKG_MAX_DIM;
+                       2 * (size_t)M * DKG_MAX_DIM + (size_t)waves * 64 + DKG_MAX_DIM +
+                       (size_t)M * DKG_MAX_DIM + (size_t)waves * (HCAP + max_np + ENV_CAP) +
+                       (size_t)(waves * HCAP + 1) / 2;
   return envelope_lds_bytes(m, N, waves, S, stream) + extra * sizeof(double);
 }
 
@@ -451,6 +474,14 @@ hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, in
                                 double diag_add, double* out, hipStream_t s) {
   dim3 grid((n2 + 255) / 256, n1);
   hipLaunchKernelGGL(kernel_matrix_kernel, grid, dim3(256), 0, s, o, d, x1, n1, x2, n2, diag_add, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, hipStream_t s) {
+  const size_t total = (size_t)rows * pad16(n);
+  if (total == 0) return hipSuccess;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(unpack_rows_kernel, dim3(blocks), dim3(256), 0, s, frag, rows, pad16(n), out);
   return hipGetLastError();
 }
 
@@ -562,7 +593,7 @@ hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xne
   }
   if (e != hipSuccess) return e;
   EnvLaunch a{&h, dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
-              envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, 0, xnew, dkg};
+              envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, h.debug_stamp, xnew, dkg};
   return launch_env<true>(h, a);
 }
 

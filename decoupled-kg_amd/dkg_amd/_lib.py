@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "
 
 ABI_VERSION = 2
 DKG_PLAN_GRAD = 1
+DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 

@@ -144,8 +144,8 @@ class DeviceGPState:
         self._ws = None
         self._ws_key = None
 
-    def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False) -> "ForwardPlan":
-        return ForwardPlan(self, W, target, max_B, grad)
+    def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False, force_walk: bool = False) -> "ForwardPlan":
+        return ForwardPlan(self, W, target, max_B, grad, force_walk)
 
     def forward(self, X: torch.Tensor, W: torch.Tensor, target, kg_pairs=None, timed: bool = False):
         """One-shot forward (builds a plan on the fly); see ForwardPlan for the fast path."""
@@ -160,7 +160,8 @@ class ForwardPlan:
     ``grad=True`` the workspace also holds the gradient buffers and
     ``forward_grad`` returns dKG/dx alongside KG."""
 
-    def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int, grad: bool = False):
+    def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int, grad: bool = False,
+                 force_walk: bool = False):
         lib = _lib.load()
         self.state = state
         self.device = state.device
@@ -171,7 +172,7 @@ class ForwardPlan:
         self.target = -1 if target is None else int(target)
         self.max_B = int(max_B)
         self.grad = bool(grad)
-        flags = _lib.DKG_PLAN_GRAD if self.grad else 0
+        flags = (_lib.DKG_PLAN_GRAD if self.grad else 0) | (_lib.DKG_PLAN_FORCE_WALK if force_walk else 0)
         need = lib.dkg_plan_workspace(state.structs, state.m, state.d, state.N, self.max_B, self.S, flags)
         self.ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
         nbytes = lib.dkg_plan_bytes()

@@ -133,6 +133,9 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
  * disc/weights/workspace buffers must outlive the plan. */
 /* Plan flags: DKG_PLAN_GRAD adds the gradient buffers (dkg_plan_forward_grad). */
 #define DKG_PLAN_GRAD 1
+/* DKG_PLAN_FORCE_WALK (test hook): the envelope stage takes its list-overflow
+ * path (gift wrap over all lines) for every pair; same results, slower. */
+#define DKG_PLAN_FORCE_WALK 2
 size_t dkg_plan_bytes(void);
 size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags);
 int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,

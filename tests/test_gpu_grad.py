@@ -138,3 +138,26 @@ def test_reference_gradcheck(ref_models, noisy, weights, target):
     else:
         fn = lambda x: calculate_discrete_kg_conditioning_on_single_output(state, x, target, disc, W)  # noqa: E731
     assert torch.autograd.gradcheck(fn, (xnew,), raise_exception=True)
+
+
+@pytest.mark.parametrize("workload", ["small", "parity6d"])
+@pytest.mark.parametrize("target", [None, 1])
+def test_overflow_walk_path_value_and_grad(workload, target):
+    """DKG_PLAN_FORCE_WALK: the envelope's list-overflow path (gift wrap over all
+    lines, discretekg.py:382-401 walk) for every pair gives the oracle's KG and gradient."""
+    model, D, X, W = make_problem(WORKLOADS[workload])
+    X, W = X[:12], W[:8]
+    om = to_oracle(model)
+    kg_ref, g_ref = oracle_grad(om, X, D, W, target)
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    tgt = -1 if target is None else target
+    Xd = X.to(DEV)
+    plan_fwd = acq._state.plan(acq._W, target, 16, force_walk=True)
+    kg = plan_fwd.forward(Xd).cpu()
+    plan_grad = acq._state.plan(acq._W, target, 16, grad=True, force_walk=True)
+    kg2, g = plan_grad.forward_grad(Xd)
+    assert tgt == plan_fwd.target
+    scale = kg_ref.abs().max().item()
+    assert (kg - kg_ref).abs().max().item() <= 1e-6 * scale + 1e-15
+    assert (kg2.cpu() - kg_ref).abs().max().item() <= 1e-6 * scale + 1e-15
+    assert_grad_close(g.cpu(), g_ref)
