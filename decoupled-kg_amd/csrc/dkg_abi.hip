@@ -1,6 +1,7 @@
 // C ABI of the Discrete-KG library (include/dkg.h).  Host-side validation,
 // workspace carving and kernel sequencing; no device work happens here.
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -253,6 +254,52 @@ int dkg_abi_version(void) { return DKG_ABI_VERSION; }
 const char* dkg_last_error(void) { return g_err.c_str(); }
 
 size_t dkg_frag_elems(int rows, int n) { return (size_t)pad16(std::max(rows, 0)) * pad16(std::max(n, 0)); }
+
+size_t dkg_prepare_workspace(int n) {
+  if (n < 1) return 0;
+  return align256((size_t)n * n * sizeof(double)) + 256;
+}
+
+int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int max_tries, double* L, void* work,
+                       size_t work_bytes, double* alpha, double* root_frag, double* jitter_used, void* stream) {
+  if (!o || !train_y || !L || !work || !alpha || !root_frag || !o->inv_lengthscale || !o->train_x)
+    return fail(DKG_ERR_ARG, "NULL pointer");
+  const int n = o->n;
+  if (n < 1) return fail(DKG_ERR_ARG, "n=%d training points", n);
+  if (pad16(n) > 1024) return fail(DKG_ERR_UNSUPPORTED, "n=%d > 1024 training points", n);
+  if (d < 1 || d > DKG_MAX_DIM) return fail(DKG_ERR_UNSUPPORTED, "d=%d (supported 1..%d)", d, DKG_MAX_DIM);
+  if (o->kernel < DKG_MATERN12 || o->kernel > DKG_RBF) return fail(DKG_ERR_ARG, "kernel id %d", o->kernel);
+  if (max_tries < 0) return fail(DKG_ERR_ARG, "max_tries=%d", max_tries);
+  if (work_bytes < dkg_prepare_workspace(n))
+    return fail(DKG_ERR_WORKSPACE, "workspace %zu bytes < required %zu", work_bytes, dkg_prepare_workspace(n));
+  hipStream_t s = (hipStream_t)stream;
+  double* X = static_cast<double*>(work);
+  int* info = reinterpret_cast<int*>(static_cast<char*>(work) + align256((size_t)n * n * sizeof(double)));
+  int st, h_info = 1;
+  double jit = 0.0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    // linear_operator psd_safe_cholesky: plain first, then absolute jitter 1e-8 * 10^i
+    jit = attempt == 0 ? 0.0 : 1e-8 * std::pow(10.0, attempt - 1);
+    if ((st = hip_check(launch_kernel_matrix(*o, d, o->train_x, n, o->train_x, n, o->noise + jit, L, s),
+                        "kernel_matrix")))
+      return st;
+    if ((st = hip_check(hipMemsetAsync(info, 0, sizeof(int), s), "hipMemsetAsync")) ||
+        (st = hip_check(launch_cholesky(L, n, info, s), "cholesky")) ||
+        (st = hip_check(hipMemcpyAsync(&h_info, info, sizeof(int), hipMemcpyDeviceToHost, s), "hipMemcpyAsync")) ||
+        (st = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize")))
+      return st;
+    if (h_info == 0) break;
+  }
+  if (h_info != 0)
+    return fail(DKG_ERR_NOT_PD, "covariance not positive definite after %d jitter retries (pivot %d)", max_tries,
+                h_info);
+  if (jitter_used) *jitter_used = jit;
+  if ((st = hip_check(launch_tri_inverse(L, X, n, info, s), "tri_inverse")) ||
+      (st = hip_check(launch_alpha(X, train_y, o->mean_constant, n, alpha, info, s), "alpha")) ||
+      (st = hip_check(launch_pack_linv(X, n, root_frag, s), "pack_linv")))
+    return st;
+  return DKG_OK;
+}
 
 int dkg_kernel_matrix(const dkg_output* o, int d, const double* x1, int n1, const double* x2, int n2,
                       double diag_add, double* out, void* stream) {

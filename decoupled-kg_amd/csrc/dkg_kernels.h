@@ -52,6 +52,13 @@ struct CrossArgs {
 hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, int n1, const double* x2, int n2,
                                 double diag_add, double* out, hipStream_t s);
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
+// State preparation (dkg_linalg.hip): blocked Cholesky with device status,
+// triangular inverse, alpha = Linv^T Linv (y - c), root_frag from Linv.
+hipError_t launch_cholesky(double* A, int n, int* info, hipStream_t s);
+hipError_t launch_tri_inverse(double* L, double* X, int n, const int* info, hipStream_t s);
+hipError_t launch_alpha(const double* X, const double* y, double c, int n, double* alpha, const int* info,
+                        hipStream_t s);
+hipError_t launch_pack_linv(const double* X, int n, double* rf, hipStream_t s);
 // Row-major copy [rows][n_pad] of a fragment-packed (rows x n) matrix.
 hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);

@@ -11,7 +11,7 @@ import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_size_t, c_void_p
 
-from .errors import BotorchTensorDimensionError, DkgNativeError, UnsupportedError
+from .errors import BotorchTensorDimensionError, DkgNativeError, NotPSDError, UnsupportedError
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdkg.so")
 
@@ -21,7 +21,8 @@ DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 
-DKG_OK, DKG_ERR_ARG, DKG_ERR_UNSUPPORTED, DKG_ERR_WORKSPACE, DKG_ERR_HIP, DKG_ERR_NO_LINES = range(6)
+(DKG_OK, DKG_ERR_ARG, DKG_ERR_UNSUPPORTED, DKG_ERR_WORKSPACE, DKG_ERR_HIP, DKG_ERR_NO_LINES,
+ DKG_ERR_NOT_PD) = range(7)
 
 
 class DkgOutput(ctypes.Structure):
@@ -52,6 +53,9 @@ SIGNATURES = {
     "dkg_kernel_matrix": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_int, c_double,
                                   c_void_p, c_void_p]),
     "dkg_pack_root": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    "dkg_prepare_workspace": (c_size_t, [c_int]),
+    "dkg_prepare_output": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_void_p, c_size_t,
+                                   c_void_p, c_void_p, POINTER(c_double), c_void_p]),
     "dkg_cross_root": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_forward_workspace": (c_size_t, [POINTER(DkgOutput), c_int, c_int, c_int, c_int]),
     "dkg_forward": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
@@ -108,6 +112,8 @@ def check(status: int, what: str) -> None:
         raise UnsupportedError(msg)
     if status == DKG_ERR_NO_LINES:
         raise ValueError(msg)
+    if status == DKG_ERR_NOT_PD:
+        raise NotPSDError(msg)
     raise DkgNativeError(msg)
 
 

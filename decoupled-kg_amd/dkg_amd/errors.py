@@ -16,8 +16,15 @@ except Exception:  # noqa: BLE001
         """Unsupported configuration (BoTorch stand-in)."""
 
 
+try:  # pragma: no cover - linear_operator is not installed in this image
+    from linear_operator.utils.errors import NotPSDError  # type: ignore
+except Exception:  # noqa: BLE001
+    class NotPSDError(RuntimeError):
+        """Covariance not positive definite after the jitter retries (linear_operator stand-in)."""
+
+
 class DkgNativeError(RuntimeError):
     """The HIP library is missing, failed to load, or reported a runtime error."""
 
 
-__all__ = ["BotorchTensorDimensionError", "UnsupportedError", "DkgNativeError"]
+__all__ = ["BotorchTensorDimensionError", "UnsupportedError", "NotPSDError", "DkgNativeError"]

@@ -4,11 +4,11 @@ Builds, per output, the caches GPyTorch's exact prediction keeps behind
 ``model.posterior`` (``discretekg.py:182-185, 275-284``) — the ones BoTorch's
 ``fast_pred_var`` posterior uses:
 
-* ``K = s k(X, X) + noise I``                 HIP ``dkg_kernel_matrix``
-* ``L = psd_safe_cholesky(K)``                torch.linalg on the GPU, with
-  linear_operator's jitter policy (absolute 1e-8 * 10**i, 3 retries)
-* ``R = L^{-T}`` (root_inv_decomposition)     torch.linalg.solve_triangular
-* ``alpha = cholesky_solve(y - c, L)``        torch.cholesky_solve
+* ``K = s k(X, X) + noise I``, ``L = psd_safe_cholesky(K)`` (linear_operator's
+  jitter policy: absolute 1e-8 * 10**i, 3 retries), ``R = L^{-T}``
+  (root_inv_decomposition) and ``alpha = K^{-1}(y - c)``:
+                                              HIP ``dkg_prepare_output`` (blocked
+                                              Cholesky / triangular inverse kernels)
 * ``root_frag`` = R in MFMA fragment order    HIP ``dkg_pack_root``
 * ``Q_D = K(D, X) R``, ``mu_D = c + K(D,X) alpha`` over the discretisation
                                               HIP ``dkg_cross_root``
@@ -38,23 +38,6 @@ def current_stream_ptr(device) -> int:
     return int(torch.cuda.current_stream(device).cuda_stream)
 
 
-def psd_safe_cholesky(A: torch.Tensor, jitter: float = 1e-8, max_tries: int = 3) -> torch.Tensor:
-    L, info = torch.linalg.cholesky_ex(A)
-    if int(info) == 0:
-        return L
-    prev = 0.0
-    Ap = A.clone()
-    eye = torch.eye(A.shape[-1], dtype=A.dtype, device=A.device)
-    for i in range(max_tries):
-        new = jitter * 10**i
-        Ap = Ap + (new - prev) * eye
-        prev = new
-        L, info = torch.linalg.cholesky_ex(Ap)
-        if int(info) == 0:
-            return L
-    raise torch.linalg.LinAlgError("covariance not positive definite after jitter retries (NotPSDError)")
-
-
 @dataclass
 class OutputCache:
     """Device tensors of one output; ``struct`` points into them."""
@@ -67,6 +50,7 @@ class OutputCache:
     disc_frag: torch.Tensor
     disc_mean: torch.Tensor
     L: torch.Tensor
+    jitter: float = 0.0  # absolute jitter psd_safe_cholesky needed (0: none)
     struct: _lib.DkgOutput = field(repr=False, default=None)
 
 
@@ -97,18 +81,16 @@ def prepare_output(st: SingleTaskGPState, D: torch.Tensor) -> OutputCache:
     inv_ls = (1.0 / st.lengthscale).to(dev).contiguous()
     o = _base_struct(st, inv_ls, X)
 
-    K = torch.empty(n, n, dtype=torch.double, device=dev)
-    _lib.check(lib.dkg_kernel_matrix(o, d, _lib.ptr(X), n, _lib.ptr(X), n, float(st.noise), _lib.ptr(K), stream),
-               "dkg_kernel_matrix")
-    L = psd_safe_cholesky(K)
-    eye = torch.eye(n, dtype=torch.double, device=dev)
-    R = torch.linalg.solve_triangular(L, eye, upper=False).mT.contiguous()
-    y = st.train_y.to(dev)
-    alpha = torch.zeros(_pad16(n), dtype=torch.double, device=dev)
-    alpha[:n] = torch.cholesky_solve((y - st.mean_constant).unsqueeze(-1), L).squeeze(-1)
-
+    y = st.train_y.to(dev).contiguous()
+    L = torch.empty(n, n, dtype=torch.double, device=dev)
+    work = torch.empty(lib.dkg_prepare_workspace(n), dtype=torch.uint8, device=dev)
+    alpha = torch.empty(_pad16(n), dtype=torch.double, device=dev)
     root_frag = torch.empty(lib.dkg_frag_elems(n, n), dtype=torch.double, device=dev)
-    _lib.check(lib.dkg_pack_root(_lib.ptr(R), n, _lib.ptr(root_frag), stream), "dkg_pack_root")
+    jitter = ctypes.c_double(0.0)
+    _lib.check(lib.dkg_prepare_output(o, d, _lib.ptr(y), 3, _lib.ptr(L), _lib.ptr(work), work.numel(),
+                                      _lib.ptr(alpha), _lib.ptr(root_frag), ctypes.byref(jitter), stream),
+               "dkg_prepare_output")
+    del work
     o.alpha = _lib.ptr(alpha)
     o.root_frag = _lib.ptr(root_frag)
 
@@ -119,7 +101,7 @@ def prepare_output(st: SingleTaskGPState, D: torch.Tensor) -> OutputCache:
                    "dkg_cross_root")
     o.disc_frag = _lib.ptr(disc_frag)
     o.disc_mean = _lib.ptr(disc_mean)
-    return OutputCache(st, inv_ls, X, alpha, root_frag, disc_frag, disc_mean, L, o)
+    return OutputCache(st, inv_ls, X, alpha, root_frag, disc_frag, disc_mean, L, jitter.value, o)
 
 
 class DeviceGPState:

@@ -49,7 +49,9 @@ enum dkg_status {
   DKG_ERR_UNSUPPORTED = 2,  /* outside supported sizes (reference: UnsupportedError) */
   DKG_ERR_WORKSPACE = 3,    /* workspace too small */
   DKG_ERR_HIP = 4,          /* HIP runtime error */
-  DKG_ERR_NO_LINES = 5      /* no lines (reference: ValueError, discretekg.py:466-470) */
+  DKG_ERR_NO_LINES = 5,     /* no lines (reference: ValueError, discretekg.py:466-470) */
+  DKG_ERR_NOT_PD = 6        /* covariance not positive definite after the jitter retries
+                               (linear_operator psd_safe_cholesky raises NotPSDError) */
 };
 
 /* Covariance families of model/factory.py:116 (ScaleKernel(base)). */
@@ -85,6 +87,29 @@ size_t dkg_frag_elems(int rows, int n);
  * GPyTorch Kernel.forward) used to build K_XX + noise I for the Cholesky. */
 int dkg_kernel_matrix(const dkg_output* o, int d, const double* x1, int n1, const double* x2, int n2,
                       double diag_add, double* out, void* stream);
+
+/* Bytes of device scratch dkg_prepare_output needs for n training points. */
+size_t dkg_prepare_workspace(int n);
+
+/* Fitted-state caches of one output computed on the device by the library's
+ * own kernels (no rocSOLVER / rocBLAS): the quantities GPyTorch's exact
+ * prediction caches behind model.posterior (discretekg.py:182-185, 275-284;
+ * gpytorch DefaultPredictionStrategy, linear_operator psd_safe_cholesky):
+ *   K = s k(X, X) + noise I (+ jitter I)
+ *   L = chol(K): blocked right-looking Cholesky; when it fails, retried with
+ *       absolute jitter 1e-8 * 10^i, i < max_tries (linear_operator's policy)
+ *   R = L^{-T} (root_inv_decomposition), packed into root_frag
+ *   alpha = K^{-1} (y - c)  (n_pad doubles, zero padded)
+ * o: n, kernel, outputscale, noise, mean_constant, inv_lengthscale, train_x
+ *    (alpha / root_frag / disc_* are ignored).  train_y: device [n] targets
+ * (model space).  L: device [n x n], receives L (row-major, zero upper
+ * triangle).  work: device scratch of dkg_prepare_workspace(n) bytes; on
+ * return it starts with L^{-1} (row-major n x n).  jitter_used (host,
+ * nullable): the absolute jitter that made K positive definite (0 if none).
+ * Synchronises `stream` once per Cholesky attempt (the retry policy reads the
+ * factorisation status).  DKG_ERR_NOT_PD if every attempt failed. */
+int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int max_tries, double* L, void* work,
+                       size_t work_bytes, double* alpha, double* root_frag, double* jitter_used, void* stream);
 
 /* Pack dense row-major R (n x n, device) into o->root_frag layout (device). */
 int dkg_pack_root(const double* r, int n, double* root_frag, void* stream);

@@ -84,3 +84,25 @@ def test_workspace_size_grows_with_problem():
     big = lib.dkg_forward_workspace(outs, 2, 1024, 128, 16)
     assert 0 < small < big
     assert big >= 2 * 128 * 1024 * 8  # the covariance rows of both outputs
+
+
+def test_prepare_output_validation_without_device():
+    lib = _lib.load()
+    assert lib.dkg_prepare_workspace(0) == 0
+    assert lib.dkg_prepare_workspace(256) >= 256 * 256 * 8
+    o = _lib.DkgOutput()
+    o.n, o.kernel = 8, 2
+    jit = ctypes.c_double(0.0)
+    # NULL device pointers -> argument error before any device work
+    assert lib.dkg_prepare_output(o, 2, None, 3, None, None, 0, None, None, ctypes.byref(jit), None) == _lib.DKG_ERR_ARG
+    o.inv_lengthscale = o.train_x = 16
+    args = (16, 3, 16, 16, lib.dkg_prepare_workspace(8), 16, 16, ctypes.byref(jit), None)
+    o.n = 2000
+    assert lib.dkg_prepare_output(o, 2, *args) == _lib.DKG_ERR_UNSUPPORTED
+    o.n = 8
+    assert lib.dkg_prepare_output(o, 17, *args) == _lib.DKG_ERR_UNSUPPORTED
+    small = (16, 3, 16, 16, 8, 16, 16, ctypes.byref(jit), None)
+    assert lib.dkg_prepare_output(o, 2, *small) == _lib.DKG_ERR_WORKSPACE
+    from dkg_amd.errors import NotPSDError
+    with pytest.raises(NotPSDError):
+        _lib.check(_lib.DKG_ERR_NOT_PD, "dkg_prepare_output")
