@@ -6,12 +6,15 @@ headline workload: m=2 outputs, n_train=256, n_disc=1024 (32x32 std grid),
 S=16 scalarisations, B=128 candidates per GPU, d=2, fp64.  Inputs and GP state
 are resident in HBM before timing.  For N>1 (torchrun, one rank per GPU,
 RCCL) each rank evaluates its own 128 candidates (weak scaling) and the
-per-candidate KG values are all-gathered every step (async, double
-buffered), so every rank ends with the whole batch.  ``--shard scalarisations``
-instead gives every rank the same 128 candidates and its own 16 weight rows
-(16*N in total) and combines per-candidate partial sums with one async RCCL
-all-reduce per step (the north-star exchange); ``value`` then
-counts headline-equivalent evals (candidates x 16 scalarisations).
+per-candidate KG values of every ``--exchange-every`` steps are all-gathered in
+one async RCCL call (double buffered), so every rank ends with the whole batch
+of every step.  ``--shard scalarisations`` instead gives every rank the same 128
+candidates and its own 16 weight rows (16*N in total) and combines the
+per-candidate partial sums with one async RCCL all-reduce per exchange (the
+north-star exchange; SURVEY.md §8(e) amortises it over K forward batches,
+count = K*B, because one collective costs about as much host and link latency as
+a whole 128-candidate forward); ``value`` then counts headline-equivalent evals
+(candidates x 16 scalarisations).
 
 Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus the
 roofline of the dominant kernel (HIP-event timed, same stream) and a bounded
@@ -40,11 +43,13 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", default="headline")
     ap.add_argument("--shard", choices=["candidates", "scalarisations"], default="candidates",
                     help="axis of the (candidate x scalarisation) space split over ranks (weak scaling)")
+    ap.add_argument("--exchange-every", type=int, default=64,
+                    help="forward batches per RCCL exchange (count = K*B fp64 values)")
     ap.add_argument("--target", type=int, default=None, help="target_output_ix (decoupled path); default full")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -127,26 +132,44 @@ def main():
     acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev)
     plan = acq._plan_for(w.B)
     Xd = X.to(dev).contiguous()
-    kgs = [torch.empty(w.B, dtype=torch.double, device=dev) for _ in range(2)]
-    gathered = [torch.empty(world * w.B, dtype=torch.double, device=dev) for _ in range(2)]
+    E = max(1, min(args.exchange_every, args.steps))
+    kbufs = [torch.empty(E, w.B, dtype=torch.double, device=dev) for _ in range(2)]
+    gathered = [torch.empty(world * E * w.B, dtype=torch.double, device=dev) for _ in range(2)]
     works = [None, None]
 
+    def exchange(slot, rows):
+        """One async RCCL collective over the first ``rows`` forward batches held in ``kbufs[slot]``."""
+        blk = kbufs[slot][:rows].view(-1)
+        if args.shard == "candidates":
+            works[slot] = dist.all_gather_into_tensor(gathered[slot][:world * rows * w.B], blk, async_op=True)
+        else:
+            blk.mul_(w.S)           # partial sums over this rank's rows; / (S*world) after the reduce
+            works[slot] = dist.all_reduce(blk, op=dist.ReduceOp.SUM, async_op=True)
+
     def step(k):
-        slot = k % 2
-        kg = kgs[slot]
-        if world > 1 and works[slot] is not None:
+        slot, row = (k // E) % 2, k % E
+        if world > 1 and row == 0 and works[slot] is not None:
             works[slot].wait()      # the exchange that last used this buffer is done
+            works[slot] = None
+        kg = kbufs[slot][row]
         plan.forward_into(Xd, kg)
-        if world > 1:
-            if args.shard == "candidates":
-                works[slot] = dist.all_gather_into_tensor(gathered[slot], kg, async_op=True)
-            else:
-                kg.mul_(w.S)        # partial sum over this rank's rows; / (S*world) after the reduce
-                works[slot] = dist.all_reduce(kg, op=dist.ReduceOp.SUM, async_op=True)
+        if world > 1 and row == E - 1:
+            exchange(slot, E)
         return kg
+
+    def flush(nsteps):
+        """Exchange the rows of a final, partially filled buffer."""
+        rem = nsteps % E
+        if world > 1 and rem:
+            exchange((nsteps // E) % 2, rem)
 
     for k in range(args.warmup):
         step(k)
+    flush(args.warmup)
+    for i, wk in enumerate(works):
+        if wk is not None:
+            wk.wait()
+            works[i] = None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -156,6 +179,7 @@ def main():
     ev0.record()
     for k in range(args.steps):
         step(k)
+    flush(args.steps)
     for wk in works:
         if wk is not None:
             wk.wait()
@@ -227,8 +251,10 @@ def main():
                        "S": w.S, "B_per_gpu": w.B, "d": w.d,
                        "path": "full" if args.target is None else f"target_output_ix={args.target}",
                        "shard": args.shard,
-                       "parallelism": f"{args.shard} sharded over {world} GPU(s); per-step async "
-                                      f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'}"},
+                       "parallelism": f"{args.shard} sharded over {world} GPU(s); one async RCCL "
+                                      f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'} "
+                                      f"per {E} forward batches",
+                       "exchange_every": E},
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
             "roofline": roof,
