@@ -66,7 +66,8 @@ def collect(args, out):
             for r in csv.DictReader(open(f)):
                 raw_rows.append(r)
                 for k, name in KERNELS.items():
-                    if k in r["Kernel_Name"]:
+                    # the forward instantiation only (envelope_kernel<MAXL, M, GRAD=false, ...>)
+                    if k in r["Kernel_Name"] and not (k == "envelope_kernel" and ", true," in r["Kernel_Name"]):
                         agg.setdefault(name, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     summary = {}
     for name, d in agg.items():
