@@ -167,6 +167,27 @@ __device__ __forceinline__ double partner_f64(double v) {
     { constexpr int S_ = 5; __VA_ARGS__ }          \
   }
 
+// v_min_f64 / v_max_f64 without the operand canonicalisation LLVM puts in
+// front of fmin/fmax (one extra VALU op per operand).  The kernels run in IEEE
+// mode, where a quiet-NaN operand yields the other operand: exactly fmin/fmax
+// for the values fed here (arithmetic results and quiet-NaN padding, never a
+// signalling NaN).
+__device__ __forceinline__ double fmin_raw(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double fmax_raw(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// c ? v : a quiet NaN (only the high word is selected: a NaN exponent with the
+// quiet bit set is a quiet NaN whatever the low word holds).
+__device__ __forceinline__ double keep_or_qnan(bool c, double v) {
+  return __hiloint2double(c ? __double2hiint(v) : 0x7FF80000, __double2loint(v));
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
   DKG_BUTTERFLY({ v = v + partner_f64<S_>(v); })
   return v;

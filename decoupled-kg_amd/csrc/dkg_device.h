@@ -139,17 +139,19 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
   // ---- extremes by value, then exact tie passes:
   // L = min b (tie: max a), R = max b (tie: max a), T = max a (tie: min b).
   // (slots beyond the line count hold padding lines: a = -inf, b = a real slope)
+  // (raw v_min/v_max: the padding lines' NaN intercepts drop out, see
+  // envelope_kernel; the tie passes select a quiet NaN for non-ties)
   double bmin = INFINITY, bmax = -INFINITY, amax = -INFINITY;
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
-    bmin = fmin(bmin, lb[t]);
-    bmax = fmax(bmax, lb[t]);
-    amax = fmax(amax, la[t]);
+    bmin = fmin_raw(bmin, lb[t]);
+    bmax = fmax_raw(bmax, lb[t]);
+    amax = fmax_raw(amax, la[t]);
   }
   DKG_BUTTERFLY({
-    bmin = fmin(bmin, partner_f64<S_>(bmin));
-    bmax = fmax(bmax, partner_f64<S_>(bmax));
-    amax = fmax(amax, partner_f64<S_>(amax));
+    bmin = fmin_raw(bmin, partner_f64<S_>(bmin));
+    bmax = fmax_raw(bmax, partner_f64<S_>(bmax));
+    amax = fmax_raw(amax, partner_f64<S_>(amax));
   })
   // short-circuit of discretekg.py:363-367 (all |b| < 1e-9), and the
   // single-slope case (one hull vertex, E = max a): KG = 0.
@@ -160,14 +162,14 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
   double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
-    aL = fmax(aL, (lb[t] == bmin) ? la[t] : -INFINITY);
-    aR = fmax(aR, (lb[t] == bmax) ? la[t] : -INFINITY);
-    bT = fmin(bT, (la[t] == amax) ? lb[t] : INFINITY);
+    aL = fmax_raw(aL, keep_or_qnan(lb[t] == bmin, la[t]));
+    aR = fmax_raw(aR, keep_or_qnan(lb[t] == bmax, la[t]));
+    bT = fmin_raw(bT, keep_or_qnan(la[t] == amax, lb[t]));
   }
   DKG_BUTTERFLY({
-    aL = fmax(aL, partner_f64<S_>(aL));
-    aR = fmax(aR, partner_f64<S_>(aR));
-    bT = fmin(bT, partner_f64<S_>(bT));
+    aL = fmax_raw(aL, partner_f64<S_>(aL));
+    aR = fmax_raw(aR, partner_f64<S_>(aR));
+    bT = fmin_raw(bT, partner_f64<S_>(bT));
   })
   const double bL = bmin, bR = bmax, aT = amax;
   f.bL = bL; f.aL = aL; f.bR = bR; f.aR = aR; f.bT = bT; f.aT = aT;
@@ -572,6 +574,20 @@ __device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const do
 // Padded length (doubles) of one LDS-staged line array: whole 1 KiB DMA pieces.
 __host__ __device__ inline int stage_len(int N) { return ((N + 127) / 128) * 128; }
 
+// Register slots per lane for a staged (non-streaming) line set of `lines`
+// lines: the envelope_kernel instantiation launch_env_bucket picks.
+__host__ __device__ inline int env_slots(int lines) {
+  return lines <= 64 * 2 ? 2 : lines <= 64 * 8 ? 8 : lines <= 64 * 17 ? 17 : 33;
+}
+
+// Stride (doubles) of one staged per-output array: room for the DMA pieces
+// and for every register slot (line k reads index k - 1; indices N ..
+// 64 * slots - 2 hold the padding lines), plus the 2-double front pad.
+__host__ __device__ inline int stage_stride(int N) {
+  const int slots = 64 * env_slots(N + 1);
+  return (stage_len(N) > slots ? stage_len(N) : slots) + 2;
+}
+
 // Async global -> LDS copy of n doubles (16 B per lane per wave instruction,
 // global_load_lds_dwordx4): the data never touches VGPRs and every piece of
 // every wave is in flight at once.  `dst` has stage_len(n) doubles of room.
@@ -620,7 +636,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   const int S = P->S;
   const int target = P->target;
   const bool full = target < 0;
-  const int SL = STREAM ? 0 : stage_len(N);
+  static_assert(STREAM || MAXL == 2 || MAXL == 8 || MAXL == 17 || MAXL == 33, "slot bucket");
   unsigned long long* st = kst_slot(dst, P, 2);
   KST_BEGIN(st);
 
@@ -637,7 +653,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   // LDS: [pad][mu_i over D] per output, [pad][cov_i over D] per output (line
   // k >= 1 reads index k - 1; the pad makes the lane-0 / slot-0 read legal),
   // the weights, then the per-wave survivor lists.
-  const int SLp = STREAM ? 0 : SL + 2;
+  const int SLp = STREAM ? 0 : stage_stride(N);
   double* lmu = smem + 2;
   double* lcv = lmu + (size_t)M * SLp;
   double* lw = lcv + (size_t)M * SLp;
@@ -724,6 +740,22 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   if (!GRAD) KST(st, 2);  // GRAD stamps: 2 preamble done, 3 filter, 4 hull, 5 gradient flush (first pair)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (!STREAM) {
+    // Padding lines k = N+1 .. 64*MAXL-1 (read at indices N .. 64*MAXL-2) come
+    // out of the branch-free line build as (a = NaN, b = b_0): mu = NaN makes
+    // the intercept NaN whatever the weights, and cov = the candidate's own
+    // variance gives line 0's slope bit for bit (same FMAs, same order).  NaN
+    // drops out of every fmin/fmax (maxNum) and fails every comparison, so the
+    // padding lines are never an extreme, a tie, a survivor or counted, and
+    // the register lines need no per-slot padding selects.
+    const int npad = 64 * MAXL - 1 - N;
+    for (int e = threadIdx.x; e < m * npad; e += blockDim.x) {
+      const int i = e / npad, idx = N + e % npad;
+      lmu[(size_t)i * SLp + idx] = __builtin_nan("");
+      if (full || i == target) lcv[(size_t)i * SLp + idx] = s_pp[i * 6 + 4];
+    }
+    __syncthreads();
+  }
   if (!GRAD) KST(st, 3);
 
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
@@ -867,17 +899,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
         la[0] = (lane == 0) ? a : la[0];
         lb[0] = (lane == 0) ? bb : lb[0];
       }
-      // padding lines beyond N (only in the last slots): never maximal, never
-      // change the min/max slope
-      const double bfill = __shfl(lb[0], 0);
-#pragma unroll
-      for (int t = 0; t < MAXL; ++t) {
-        if (64 * t + 63 > N) {  // wave-uniform
-          const bool pad = lane + 64 * t > N;
-          la[t] = pad ? -INFINITY : la[t];
-          lb[t] = pad ? bfill : lb[t];
-        }
-      }
+      // padding lines beyond N: (NaN, b_0) from the padded staging (see above)
     };
 
     double kgj;

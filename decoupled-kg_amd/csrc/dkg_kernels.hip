@@ -402,7 +402,7 @@ static int outputs_bucket(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 3 ? 3 :
 
 size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream) {
   const int M = outputs_bucket(m);
-  const size_t staged = stream ? 0 : 2 * (size_t)M * (stage_len(N) + 2);
+  const size_t staged = stream ? 0 : 2 * (size_t)M * stage_stride(N);
   return ((size_t)2 + staged + ((S * m + 1) & ~1) + (size_t)waves * 2 * ENV_CAP) * sizeof(double);
 }
 
