@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix
 HBM_PEAK_GBS = 8000.0
 
 
@@ -51,6 +52,8 @@ def parse():
     ap.add_argument("--exchange-every", type=int, default=64,
                     help="forward batches per RCCL exchange (count = K*B fp64 values)")
     ap.add_argument("--target", type=int, default=None, help="target_output_ix (decoupled path); default full")
+    ap.add_argument("--precision", choices=["fp64", "fp32"], default="fp64",
+                    help="fp32: the contractions in fp32 MFMA (DKG_PLAN_F32; BASELINE configs[4], workload stress32)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-reps", type=int, default=50)
@@ -129,7 +132,8 @@ def main():
         # weak scaling: S rows per rank out of S*world (rank 0's rows are the headline W)
         W_all = W if world == 1 else torch.cat([W, sample_simplex(w.m, w.S * (world - 1), qmc=True, seed=99)])
         W_local = W_all[rank * w.S:(rank + 1) * w.S]
-    acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev)
+    acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev,
+                                    precision=args.precision)
     plan = acq._plan_for(w.B)
     Xd = X.to(dev).contiguous()
     E = max(1, min(args.exchange_every, args.steps))
@@ -203,7 +207,8 @@ def main():
     fl, by = model_fb[names[dom]]
     # every stage is fp64-compute bound (DESIGN.md "Roofline"): MFMA for cross/cov, fp64 VALU (same 78.6 TF
     # peak) for the envelope; HBM bytes per launch are << peak*duration for all three.
-    bound, ach, peak, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
+    peak = FP32_MFMA_PEAK_TFLOPS if (args.precision == "fp32" and dom < 2) else FP64_PEAK_TFLOPS
+    bound, ach, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, "TFLOP/s"
     traffic = None
     if os.path.exists(args.pmc):
         try:
@@ -217,7 +222,7 @@ def main():
 
     # ---- value + gradient (dkg_plan_forward_grad: the optimize_acqf L-BFGS-B path), same batch
     grad_info = None
-    if args.grad_steps > 0:
+    if args.grad_steps > 0 and args.precision == "fp64":
         gplan = acq._plan_for(w.B, grad=True)
         for _ in range(3):
             gplan.forward_grad(Xd)
@@ -245,8 +250,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: seeded GP-prior draw, lengthscales family (l=0.2/1.8, s=1/50, noise 1e-4)",
+            "dtype": "f64" if args.precision == "fp64" else "f32 contractions / f64 envelope",
+            "data": f"synthetic: seeded GP-prior draw, lengthscales family ({w.lengthscales}, s={w.outputscales}, "
+                    f"noise {'%g x s' % w.noise_rel if w.noise_rel > 0 else w.noise})",
             "config": {"workload": args.workload, "m": w.m, "n_train": w.n_train, "n_disc": D.shape[0],
                        "S": w.S, "B_per_gpu": w.B, "d": w.d,
                        "path": "full" if args.target is None else f"target_output_ix={args.target}",

@@ -39,6 +39,7 @@ struct WsLayout {
   size_t qxrm[DKG_MAX_OUTPUTS];
   size_t qdrm[DKG_MAX_OUTPUTS];
   size_t q[DKG_MAX_OUTPUTS];
+  size_t q32[DKG_MAX_OUTPUTS], root32[DKG_MAX_OUTPUTS], disc32[DKG_MAX_OUTPUTS];
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
   size_t cov[DKG_MAX_OUTPUTS];
@@ -65,6 +66,15 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
     }
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
+    if (flags & DKG_PLAN_F32) {
+      const size_t np = pad16(outs[i].n);
+      L.q32[i] = off;
+      off = align256(off + Bp * np * sizeof(float));
+      L.root32[i] = off;
+      off = align256(off + np * np * sizeof(float));
+      L.disc32[i] = off;
+      off = align256(off + (size_t)pad16(std::max(N, 1)) * np * sizeof(float));
+    }
   }
   // contiguous per-output blocks (the envelope stage addresses them from
   // kernel-argument base pointers): means and variances at the candidates
@@ -132,7 +142,10 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
-  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK)) return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
+  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK | DKG_PLAN_F32))
+    return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
+  if (want_grad && (flags & DKG_PLAN_F32))
+    return fail(DKG_ERR_UNSUPPORTED, "the fp32 plan (DKG_PLAN_F32) is forward only; the gradient runs in fp64");
   if (want_grad && envelope_grad_lds_bytes(m, N, sw, S, d, max_np, true) > 160 * 1024)
     return fail(DKG_ERR_UNSUPPORTED, "gradient: m=%d outputs, n=%d, d=%d exceed the envelope stage's LDS", m, max_np,
                 d);
@@ -153,6 +166,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->disc = (N > 0) ? disc : reinterpret_cast<const double*>(ws);  // always a readable address
   P->weights = weights;
   P->grad = want_grad ? 1 : 0;
+  P->f32 = (flags & DKG_PLAN_F32) ? 1 : 0;
   P->stream = stream ? 1 : 0;
   P->bpad = pad16(std::max(max_B, 1));
   for (int i = 0; i < m; ++i) {
@@ -165,6 +179,11 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
       P->qdrm[i] = reinterpret_cast<double*>(ws + L.qdrm[i]);
     }
     P->q[i] = reinterpret_cast<double*>(ws + L.q[i]);
+    if (flags & DKG_PLAN_F32) {
+      P->q32[i] = reinterpret_cast<float*>(ws + L.q32[i]);
+      P->root32[i] = reinterpret_cast<float*>(ws + L.root32[i]);
+      P->disc32[i] = reinterpret_cast<float*>(ws + L.disc32[i]);
+    }
     P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
     P->var[i] = reinterpret_cast<double*>(ws + L.var[i]);
     P->cov[i] = reinterpret_cast<double*>(ws + L.cov[i]);
@@ -216,6 +235,14 @@ size_t plan_slot_bytes() { return align256(sizeof(Plan)); }
 
 // mu_D of every output into the plan's contiguous [m][N] block (stream ordered).
 int copy_disc_means(const Plan& P, hipStream_t s) {
+  for (int i = 0; i < P.m && P.f32; ++i) {
+    // F32: fp32 copies of R^T and Q_D for the fp32 contractions
+    int st = hip_check(launch_frag_to_f32(P.o[i].root_frag, P.o[i].n, P.o[i].n, P.root32[i], s), "frag_to_f32(R)");
+    if (st) return st;
+    if (P.N > 0 &&
+        (st = hip_check(launch_frag_to_f32(P.o[i].disc_frag, P.N, P.o[i].n, P.disc32[i], s), "frag_to_f32(Q_D)")))
+      return st;
+  }
   for (int i = 0; i < P.m && P.N > 0; ++i) {
     int st = hip_check(hipMemcpyAsync(P.mu_all + (size_t)i * P.N, P.o[i].disc_mean, sizeof(double) * P.N,
                                       hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(mu_D)");

@@ -40,6 +40,23 @@ __device__ __forceinline__ double2 frag_pair(const double* __restrict__ base, in
   return reinterpret_cast<const double2*>(base)[((size_t)tile * (KB >> 1) + j) * 64 + lane];
 }
 
+// fp32 form (DKG_PLAN_F32): v_mfma_f32_16x16x4_f32 has the same A/B lane maps
+// as the f64 instruction above, so the same fragment order serves, but its D
+// map differs: lane l, register r holds D[4 (l >> 4) + r][l & 15].  Four
+// consecutive k-blocks share one aligned 16-byte word ("quad-packed"):
+// element (16 t + (l & 15), 4 kb + (l >> 4)) at ((t * KB/4 + kb/4) * 64 + l) * 4 + (kb & 3).
+typedef float f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4 mfma_f32(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__host__ __device__ inline size_t frag32_index(int t, int kb, int l, int KB) {
+  return (((size_t)t * (KB >> 2) + (kb >> 2)) * 64 + l) * 4 + (kb & 3);
+}
+// Lane's operands of k-blocks 4 j .. 4 j + 3 of tile `tile`.
+__device__ __forceinline__ float4 frag_quad(const float* __restrict__ base, int tile, int j, int lane, int KB) {
+  return reinterpret_cast<const float4*>(base)[((size_t)tile * (KB >> 2) + j) * 64 + lane];
+}
+
 // Kernel profile of ScaleKernel(base) at squared scaled distance r2:
 // gpytorch MaternKernel.forward / RBFKernel (factory.py:116 catalog).
 __device__ __forceinline__ double kernel_profile(int kind, double r2) {

@@ -19,7 +19,7 @@ struct Plan {
   int32_t grad;                     // workspace holds the gradient buffers (DKG_PLAN_GRAD)
   int32_t bpad;                     // pad16(max_B): rows of the fragment-packed candidate buffers
   int32_t stream;                   // envelope streams the lines from global memory (large N)
-  int32_t pad2_;
+  int32_t f32;                      // DKG_PLAN_F32: fp32 contractions (q32 / root32 / disc32)
   const double* disc;               // [N x d]
   const double* weights;            // [S x m]
   double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
@@ -38,6 +38,9 @@ struct Plan {
   int64_t cov_stride;               // max_B * N
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
   int* tickets;                     // [B] arrival counters (split > 2 only)
+  float* q32[DKG_MAX_OUTPUTS];      // F32: quad-packed K(x, X) R per output (workspace)
+  float* root32[DKG_MAX_OUTPUTS];   // F32: quad-packed R^T (fp32 copy of root_frag, plan init)
+  float* disc32[DKG_MAX_OUTPUTS];   // F32: quad-packed Q_D (fp32 copy of disc_frag, plan init)
 };
 
 // By-value arguments of the state-preparation use of the cross stage.
@@ -59,6 +62,8 @@ hipError_t launch_tri_inverse(double* L, double* X, int n, const int* info, hipS
 hipError_t launch_alpha(const double* X, const double* y, double c, int n, double* alpha, const int* info,
                         hipStream_t s);
 hipError_t launch_pack_linv(const double* X, int n, double* rf, hipStream_t s);
+// fp32 quad-packed copy (frag32_index) of a pair-packed fp64 (rows x n) matrix.
+hipError_t launch_frag_to_f32(const double* frag, int rows, int n, float* out, hipStream_t s);
 // Row-major copy [rows][n_pad] of a fragment-packed (rows x n) matrix.
 hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);

@@ -51,6 +51,54 @@ __global__ void unpack_rows_kernel(const double* __restrict__ frag, int rows, in
   }
 }
 
+// fp32 quad-packed copy of a pair-packed fp64 fragment matrix (rows_pad x np):
+// one thread per fp32 element, coalesced stores (DKG_PLAN_F32 plan init).
+__global__ void frag_to_f32_kernel(const double* __restrict__ frag, int rows_pad, int np, float* __restrict__ out) {
+  const int KB = np / 4;
+  const size_t total = (size_t)rows_pad * np;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e & 3);
+    const size_t rest = e >> 2;
+    const int l = (int)(rest & 63);
+    const size_t blk = rest >> 6;
+    const int kb = 4 * (int)(blk % (KB / 4)) + r;
+    const int t = (int)(blk / (KB / 4));
+    out[e] = (float)frag[frag_index(t, kb, l, KB)];
+  }
+}
+
+// Element-type plumbing of the two contractions (T = double: the reference's
+// fp64; T = float: DKG_PLAN_F32): accumulator vector, MFMA, fragment words.
+template <class T> struct AccT;
+template <> struct AccT<double> { typedef d4 type; };
+template <> struct AccT<float> { typedef f4 type; };
+__device__ __forceinline__ d4 mfma_t(double a, double b, d4 c) { return mfma_f64(a, b, c); }
+__device__ __forceinline__ f4 mfma_t(float a, float b, f4 c) { return mfma_f32(a, b, c); }
+// k-blocks per 16-byte fragment word
+template <class T> constexpr int kpack() { return sizeof(T) == 8 ? 2 : 4; }
+template <class T>
+__host__ __device__ inline size_t fragT_index(int t, int kb, int l, int KB) {
+  if constexpr (sizeof(T) == 8) return frag_index(t, kb, l, KB);
+  else return frag32_index(t, kb, l, KB);
+}
+// Row of the 16x16 MFMA result held by lane l in accumulator register r.
+template <class T>
+__device__ __forceinline__ int mfma_drow(int l, int r) {
+  if constexpr (sizeof(T) == 8) return (l >> 4) + 4 * r;
+  else return 4 * (l >> 4) + r;
+}
+// lane's operands of the kpack<T>() k-blocks of word j of tile `tile` into out[0 ..)
+template <class T>
+__device__ __forceinline__ void frag_word(const T* __restrict__ base, int tile, int j, int lane, int KB, T* out) {
+  if constexpr (sizeof(T) == 8) {
+    const double2 v = frag_pair(base, tile, j, lane, KB);
+    out[0] = v.x; out[1] = v.y;
+  } else {
+    const float4 v = frag_quad(base, tile, j, lane, KB);
+    out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // cross_root_kernel: one workgroup per (16-row tile ti, tile pair p, output).
 // The pair is (p, T-1-p) of 16-column tiles of Q = K_x R; R upper triangular
@@ -65,12 +113,18 @@ constexpr int CR_U = 8;  // k-blocks per load batch
 
 // GRAD: the same contraction with the kernel replaced by its derivative in
 // the candidate's coordinate `gdim` (J = dK(x, X)/dx_g R, dmean = dK/dx_g alpha).
-template <int DM, bool GRAD = false>
+// T = float (DKG_PLAN_F32): R^T and Q in fp32 (quad-packed), fp32 MFMA; the
+// kernel evaluations and the mean stay fp64.
+template <int DM, bool GRAD = false, class ET = double>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
-                                                double* __restrict__ qout, double* __restrict__ mout, int ti, int p,
+                                                ET* __restrict__ qout, double* __restrict__ mout, int ti, int p,
                                                 double* smem, unsigned long long* st = nullptr, int gdim = 0,
                                                 const double* __restrict__ qx_frag = nullptr,
-                                                double* __restrict__ qx_rm = nullptr) {
+                                                double* __restrict__ qx_rm = nullptr,
+                                                const ET* __restrict__ root = nullptr) {
+  static_assert(!GRAD || sizeof(ET) == 8, "the gradient stage is fp64");
+  constexpr int QW = kpack<ET>();
+  if constexpr (sizeof(ET) == 8) root = o.root_frag;
   const int n = o.n;
   const int np = pad16(n);
   const int T = np / 16;
@@ -84,7 +138,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  double* kb_lds = smem;                         // [KB][64]
+  ET* kb_lds = reinterpret_cast<ET*>(smem);        // [KB][64]
   double* part = smem;                           // [CR_WAVES][8][64], overlays kb_lds once the MFMAs are done
   double* mred = smem + max(KB * 64, CR_WAVES * 8 * 64);  // [CR_WAVES][16]
   double* xs = mred + CR_WAVES * 16;             // [np][d] staged training inputs
@@ -93,17 +147,15 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   // R fragments of this wave's first k-block batch: loaded before anything
   // else so their latency overlaps the staging and the kernel evaluations.
   // (k-block ranges are even: kbA, kbB are multiples of 4 and chunk is even)
-  const int chunk = 2 * ((kbB / 2 + CR_WAVES - 1) / CR_WAVES);
+  const int chunk = QW * ((kbB / QW + CR_WAVES - 1) / CR_WAVES);
   const int k0 = wave * chunk;
   const int k1 = min(kbB, k0 + chunk);
-  double ra[CR_U], rb[CR_U];
+  ET ra[CR_U], rb[CR_U];
 #pragma unroll
-  for (int u = 0; u < CR_U; u += 2) {
-    const int j = min(k0 + u, kbB - 2) >> 1;
-    const double2 vb = frag_pair(o.root_frag, tB, j, lane, KB);
-    const double2 va = frag_pair(o.root_frag, tA, min(j, kbA / 2 - 1), lane, KB);
-    rb[u] = vb.x; rb[u + 1] = vb.y;
-    ra[u] = va.x; ra[u + 1] = va.y;
+  for (int u = 0; u < CR_U; u += QW) {
+    const int j = min(k0 + u, kbB - QW) / QW;
+    frag_word<ET>(root, tB, j, lane, KB, rb + u);
+    frag_word<ET>(root, tA, min(j, kbA / QW - 1), lane, KB, ra + u);
   }
 
   KST(st, 2);
@@ -157,7 +209,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       const double v = (rv && col < n) ? kv : 0.0;
       const double al = als[cc];  // staged only when want_mean; otherwise ignored
       mpart = fma(v, want_mean ? al : 0.0, mpart);
-      if (e < fill) kb_lds[e] = v;
+      if (e < fill) kb_lds[e] = (ET)v;
     }
   };
   switch (o.kernel) {
@@ -170,39 +222,38 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
 
   KST(st, 4);
   // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
-  d4 accA2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-  d4 accB2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  typedef typename AccT<ET>::type acc_t;
+  acc_t accA2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  acc_t accB2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   const bool pairA = tA != tB;
   for (int base = k0; base < k1; base += CR_U) {
-    double bo[CR_U];
+    ET bo[CR_U];
     if (base != k0) {
 #pragma unroll
-      for (int u = 0; u < CR_U; u += 2) {
-        const int j = min(base + u, kbB - 2) >> 1;
-        const double2 vb = frag_pair(o.root_frag, tB, j, lane, KB);
-        const double2 va = frag_pair(o.root_frag, tA, min(j, kbA / 2 - 1), lane, KB);
-        rb[u] = vb.x; rb[u + 1] = vb.y;
-        ra[u] = va.x; ra[u + 1] = va.y;
+      for (int u = 0; u < CR_U; u += QW) {
+        const int j = min(base + u, kbB - QW) / QW;
+        frag_word<ET>(root, tB, j, lane, KB, rb + u);
+        frag_word<ET>(root, tA, min(j, kbA / QW - 1), lane, KB, ra + u);
       }
     }
 #pragma unroll
     for (int u = 0; u < CR_U; ++u) {
       const int kb = min(base + u, kbB - 1);
-      bo[u] = (base + u < k1) ? kb_lds[kb * 64 + lane] : 0.0;
+      bo[u] = (base + u < k1) ? kb_lds[kb * 64 + lane] : (ET)0;
     }
 #pragma unroll
     for (int u = 0; u < CR_U; ++u) {
-      accB2[u & 1] = mfma_f64(rb[u], bo[u], accB2[u & 1]);
-      if (pairA && base + u < kbA) accA2[u & 1] = mfma_f64(ra[u], bo[u], accA2[u & 1]);
+      accB2[u & 1] = mfma_t(rb[u], bo[u], accB2[u & 1]);
+      if (pairA && base + u < kbA) accA2[u & 1] = mfma_t(ra[u], bo[u], accA2[u & 1]);
     }
   }
-  const d4 accA = accA2[0] + accA2[1];
-  const d4 accB = accB2[0] + accB2[1];
+  const acc_t accA = accA2[0] + accA2[1];
+  const acc_t accB = accB2[0] + accB2[1];
   __syncthreads();  // every wave is done with kb_lds before the partials overwrite it
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    part[(wave * 8 + r) * 64 + lane] = accA[r];
-    part[(wave * 8 + 4 + r) * 64 + lane] = accB[r];
+    part[(wave * 8 + r) * 64 + lane] = (double)accA[r];
+    part[(wave * 8 + 4 + r) * 64 + lane] = (double)accB[r];
   }
   // mean partials: lanes l, l^16, l^32, l^48 share a row.
   if (want_mean) {
@@ -230,7 +281,9 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
         qout[rm] = s;
         if (qx_rm) qx_rm[rm] = qx_frag[frag_index(ti, 4 * tj + r, lane, KB)];
       } else {
-        qout[frag_index(ti, 4 * tj + r, lane, KB)] = s;
+        // D row dr = column 16 tj + dr of Q: k-block 4 tj + dr/4, operand lane (l & 15) | (dr % 4) << 4
+        const int dr = mfma_drow<ET>(lane, r);
+        qout[fragT_index<ET>(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = (ET)s;
       }
     }
   }
@@ -252,7 +305,7 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a
 
 // Forward: grid (B tiles, pairs, outputs); workgroup (0,0,0) also clears the
 // KG accumulators (and arrival tickets) the envelope stage adds into.
-template <int DM>
+template <int DM, class T = double>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const Plan* __restrict__ P,
                                                                           const double* __restrict__ xnew, int B,
                                                                           double* __restrict__ kg, int dst) {
@@ -266,7 +319,12 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
       if (P->split > 2) P->tickets[i] = 0;
     }
   }
-  cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
+  if constexpr (sizeof(T) == 8) {
+    cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
+  } else {
+    cross_root_impl<DM, false, float>(P->o[oi], P->d, xnew, B, P->q32[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem,
+                                      st, 0, nullptr, nullptr, P->root32[oi]);
+  }
 }
 
 // Gradient cross stage: grid (B tiles, pairs, outputs x d); z = oi * d + g
@@ -304,10 +362,15 @@ size_t cross_root_lds_bytes(int np, int d) {
 constexpr int PC_WAVES = 8;
 constexpr int PC_P = 8;  // 16-byte pairs per operand per load batch (16 k-blocks)
 
-template <int DM>
+// T = float (DKG_PLAN_F32): the contraction Q_X . Q_D in fp32 (quad-packed
+// operands, v_mfma_f32_16x16x4_f32); the kernel term, the subtraction and the
+// variance sums (of the fp32 Q_X entries) in fp64.
+template <int DM, class T = double>
 __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
                                                                          const double* __restrict__ xnew, int B,
                                                                          int dst) {
+  constexpr int QW = kpack<T>();
+  typedef typename AccT<T>::type acc_t;
   __shared__ __attribute__((aligned(16))) double part[4 * 4 * 64];  // K-half 1 partial tiles
   __shared__ double qpart[4 * 16];
   unsigned long long* st = kst_slot(dst, P, 1);
@@ -325,9 +388,18 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   // tiles that exist in the workspace / state buffers (wave-uniform)
   const bool live = ti * 16 < pad16(B) && (tk * 16 < pad16(N) || (tk == 0 && !have_d));
   const bool want_var = tk == 0;
-  // K-half of this wave, in whole 16-byte pairs
-  const int KP = KB / 2;
+  // K-half of this wave, in whole 16-byte words (QW k-blocks each)
+  const int KP = KB / QW;
   const int p0 = half * ((KP + 1) / 2), p1 = half ? KP : (KP + 1) / 2;
+  const T* qx;
+  const T* qd;
+  if constexpr (sizeof(T) == 8) {
+    qx = P->q[oi];
+    qd = o.disc_frag;
+  } else {
+    qx = P->q32[oi];
+    qd = P->disc32[oi];
+  }
 
   // epilogue operands first (row b = 16 ti + (l >> 4) + 4 r, column k = 16 tk + (l & 15))
   const int d = P->d;
@@ -337,38 +409,39 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int b = ti * 16 + (lane >> 4) + 4 * r;
+      const int b = ti * 16 + mfma_drow<T>(lane, r);
       r2[r] = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d);
     }
   }
   KST(st, 2);
-  d4 acc[4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  acc_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
   double qsq = 0.0;  // lane l: sum over this wave's k of Q_X[16 ti + (l & 15)][k]^2
   if (live) {
     for (int pb = p0; pb < p1; pb += PC_P) {
-      double2 va[PC_P], vd[PC_P];
-      // disc_frag tile 0 exists only when N > 0: the N == 0 variance-only
+      T va[PC_P][QW], vd[PC_P][QW];
+      // disc_frag tile 0 exists only when N == 0: the N == 0 variance-only
       // wave reads its own Q_X tile as a stand-in (multiplied by 0 below)
-      const double* dsrc = have_d ? o.disc_frag : P->q[oi];
+      const T* dsrc = have_d ? qd : qx;
       const int dt = have_d ? tk : ti;
 #pragma unroll
       for (int u = 0; u < PC_P; ++u) {
         const int j = min(pb + u, p1 - 1);
-        va[u] = frag_pair(P->q[oi], ti, j, lane, KB);
-        vd[u] = frag_pair(dsrc, dt, j, lane, KB);
+        frag_word<T>(qx, ti, j, lane, KB, va[u]);
+        frag_word<T>(dsrc, dt, j, lane, KB, vd[u]);
       }
 #pragma unroll
       for (int u = 0; u < PC_P; ++u) {
         const bool in = pb + u < p1 && have_d;
-        const double a0 = va[u].x, a1 = va[u].y;
-        const double d0 = in ? vd[u].x : 0.0, d1 = in ? vd[u].y : 0.0;
-        acc[(2 * u) & 3] = mfma_f64(a0, d0, acc[(2 * u) & 3]);
-        acc[(2 * u + 1) & 3] = mfma_f64(a1, d1, acc[(2 * u + 1) & 3]);
-        if (want_var) qsq = (pb + u < p1) ? fma(a1, a1, fma(a0, a0, qsq)) : qsq;
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const T a = va[u][q], dd = in ? vd[u][q] : (T)0;
+          acc[(QW * u + q) & 3] = mfma_t(a, dd, acc[(QW * u + q) & 3]);
+          if (want_var) qsq = (pb + u < p1) ? fma((double)a, (double)a, qsq) : qsq;
+        }
       }
     }
   }
-  const d4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  const acc_t accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   KST(st, 3);
   if (want_var) {
     qsq += __shfl_xor(qsq, 16);
@@ -376,7 +449,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   }
   if (half == 1) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) part[(tt * 4 + r) * 64 + lane] = accs[r];
+    for (int r = 0; r < 4; ++r) part[(tt * 4 + r) * 64 + lane] = (double)accs[r];
     if (want_var && lane < 16) qpart[tt * 16 + lane] = qsq;
   }
   __syncthreads();
@@ -384,8 +457,8 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   if (half == 0 && live) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const double sum = accs[r] + part[(tt * 4 + r) * 64 + lane];
-      const int b = ti * 16 + (lane >> 4) + 4 * r;
+      const double sum = (double)accs[r] + part[(tt * 4 + r) * 64 + lane];
+      const int b = ti * 16 + mfma_drow<T>(lane, r);
       if (b < B && k < N)
         P->cov[oi][(size_t)b * N + k] =
             o.outputscale * kernel_profile(o.kernel, r2[r]) - sum;
@@ -485,6 +558,14 @@ hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, 
   return hipGetLastError();
 }
 
+hipError_t launch_frag_to_f32(const double* frag, int rows, int n, float* out, hipStream_t s) {
+  const size_t total = (size_t)pad16(rows) * pad16(n);
+  if (total == 0) return hipSuccess;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(frag_to_f32_kernel, dim3(blocks), dim3(256), 0, s, frag, pad16(rows), pad16(n), out);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s) {
   const size_t total = (size_t)pad16(n) * pad16(n);
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
@@ -512,22 +593,29 @@ hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s) {
   }
 }
 
-template <int DM>
-static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
-                                     hipStream_t s, int stage) {
+template <int DM, class T>
+static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
+                                      hipStream_t s, int stage) {
   if (stage == 0) {
     dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
     if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
-    hipLaunchKernelGGL(cross_root_plan_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
+      (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel<DM, T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((cross_root_plan_kernel<DM, T>), grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
                        h.debug_stamp);
     return hipGetLastError();
   }
   dim3 grid(std::max(1, (h.N + 31) / 32), (B + 31) / 32, h.m);
-  hipLaunchKernelGGL(posterior_cov_kernel<DM>, grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B, h.debug_stamp);
+  hipLaunchKernelGGL((posterior_cov_kernel<DM, T>), grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B, h.debug_stamp);
   return hipGetLastError();
+}
+
+template <int DM>
+static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
+                                     hipStream_t s, int stage) {
+  return h.f32 ? launch_cross_cov_tt<DM, float>(h, dev, xnew, B, kg, s, stage)
+               : launch_cross_cov_tt<DM, double>(h, dev, xnew, B, kg, s, stage);
 }
 
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {

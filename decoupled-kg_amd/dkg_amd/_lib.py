@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "
 ABI_VERSION = 2
 DKG_PLAN_GRAD = 1
 DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
+DKG_PLAN_F32 = 4  # fp32 contractions (BASELINE configs[4]); forward only
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 

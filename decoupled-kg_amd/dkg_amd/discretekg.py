@@ -105,7 +105,7 @@ class DiscreteKnowledgeGradient(_Base):
         return cls(model, x_disc, scalarisation_weights, target_output_ix)
 
     def __init__(self, model, x_discretisation: Tensor, scalarisation_weights: Optional[Tensor] = None,
-                 target_output_ix: Optional[int] = None, device=None):
+                 target_output_ix: Optional[int] = None, device=None, precision: str = "fp64"):
         if _HAVE_BOTORCH:  # pragma: no cover
             super().__init__(model=model)
         else:
@@ -134,6 +134,11 @@ class DiscreteKnowledgeGradient(_Base):
         if target_output_ix is not None and not (0 <= int(target_output_ix) < state.num_outputs):
             raise BotorchTensorDimensionError(
                 f"target_output_ix={target_output_ix} out of range for {state.num_outputs} outputs")
+        if precision not in ("fp64", "fp32"):
+            raise ValueError(f"precision must be 'fp64' (the reference's) or 'fp32', got {precision!r}")
+        # "fp32": the two contractions of the forward in fp32 MFMA (include/dkg.h DKG_PLAN_F32;
+        # BASELINE configs[4]); not a reference mode, forward only
+        self.precision = precision
         self.x_discretisation = x_discretisation
         self.scalarisation_weights = scalarisation_weights
         self.target_output_ix = target_output_ix
@@ -149,7 +154,10 @@ class DiscreteKnowledgeGradient(_Base):
             cap = 1
             while cap < B:
                 cap *= 2
-            cur = self._state.plan(self._W, self.target_output_ix, max(cap, 16), grad=grad)
+            if grad and self.precision == "fp32":
+                raise UnsupportedError("precision='fp32' is forward only; use precision='fp64' for gradients")
+            cur = self._state.plan(self._W, self.target_output_ix, max(cap, 16), grad=grad,
+                                   f32=self.precision == "fp32")
             if grad:
                 self._plan_grad = cur
             else:

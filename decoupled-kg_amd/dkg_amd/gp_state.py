@@ -126,8 +126,9 @@ class DeviceGPState:
         self._ws = None
         self._ws_key = None
 
-    def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False, force_walk: bool = False) -> "ForwardPlan":
-        return ForwardPlan(self, W, target, max_B, grad, force_walk)
+    def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False, force_walk: bool = False,
+             f32: bool = False) -> "ForwardPlan":
+        return ForwardPlan(self, W, target, max_B, grad, force_walk, f32)
 
     def forward(self, X: torch.Tensor, W: torch.Tensor, target, kg_pairs=None, timed: bool = False):
         """One-shot forward (builds a plan on the fly); see ForwardPlan for the fast path."""
@@ -143,7 +144,7 @@ class ForwardPlan:
     ``forward_grad`` returns dKG/dx alongside KG."""
 
     def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int, grad: bool = False,
-                 force_walk: bool = False):
+                 force_walk: bool = False, f32: bool = False):
         lib = _lib.load()
         self.state = state
         self.device = state.device
@@ -154,7 +155,9 @@ class ForwardPlan:
         self.target = -1 if target is None else int(target)
         self.max_B = int(max_B)
         self.grad = bool(grad)
-        flags = (_lib.DKG_PLAN_GRAD if self.grad else 0) | (_lib.DKG_PLAN_FORCE_WALK if force_walk else 0)
+        self.f32 = bool(f32)
+        flags = ((_lib.DKG_PLAN_GRAD if self.grad else 0) | (_lib.DKG_PLAN_FORCE_WALK if force_walk else 0)
+                 | (_lib.DKG_PLAN_F32 if self.f32 else 0))
         need = lib.dkg_plan_workspace(state.structs, state.m, state.d, state.N, self.max_B, self.S, flags)
         self.ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
         nbytes = lib.dkg_plan_bytes()

@@ -33,6 +33,7 @@ class Workload:
     lengthscales: tuple = (0.2, 1.8)
     outputscales: tuple = (1.0, 50.0)
     noise: float = 1e-4
+    noise_rel: float = 0.0  # > 0: noise of output i = noise_rel * outputscale_i (overrides `noise`)
 
     @property
     def n_disc(self) -> int:
@@ -50,6 +51,10 @@ WORKLOADS = {
     # BASELINE.json configs[4] (the stress config; computed in fp64 here)
     "stress": Workload("stress", m=3, n_train=1024, grid=64, S=32, B=256,
                        lengthscales=(0.2, 1.8, 0.6), outputscales=(1.0, 50.0, 5.0), noise=1e-3),
+    # BASELINE.json configs[4] as specified for fp32 (noise >= 1e-3 of the outputscale), the
+    # workload of the DKG_PLAN_F32 path
+    "stress32": Workload("stress32", m=3, n_train=1024, grid=64, S=32, B=256,
+                         lengthscales=(0.2, 1.8, 0.6), outputscales=(1.0, 50.0, 5.0), noise_rel=1e-3),
 }
 
 
@@ -67,9 +72,10 @@ def make_problem(w: Workload, seed: int = 0):
     for i in range(w.m):
         ls = w.lengthscales[i % len(w.lengthscales)]
         s = w.outputscales[i % len(w.outputscales)]
-        K = _matern52(X, X, ls, s) + w.noise * torch.eye(w.n_train, dtype=dt)
+        noise = w.noise_rel * s if w.noise_rel > 0 else w.noise
+        K = _matern52(X, X, ls, s) + noise * torch.eye(w.n_train, dtype=dt)
         y = torch.linalg.cholesky(K) @ torch.randn(w.n_train, generator=g, dtype=dt)
-        outs.append(SingleTaskGPState(X, y, ls, s, w.noise, 0.0))
+        outs.append(SingleTaskGPState(X, y, ls, s, noise, 0.0))
     model = ModelListGPState(*outs)
     if w.d <= 3:
         D = make_torch_std_grid(w.grid, w.d, {"dtype": dt})

@@ -161,6 +161,15 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
 /* DKG_PLAN_FORCE_WALK (test hook): the envelope stage takes its list-overflow
  * path (gift wrap over all lines) for every pair; same results, slower. */
 #define DKG_PLAN_FORCE_WALK 2
+/* DKG_PLAN_F32: the two contractions of the forward (Q_X = K(x,X) R and
+ * Q_X . Q_D, BASELINE configs[4]'s "fp32 MFMA-bound stress") run in fp32 on
+ * v_mfma_f32_16x16x4_f32 over fp32 copies of R and Q_D made at plan init; the
+ * kernel evaluations, means, variances (fp64 sums of the fp32 Q_X squares),
+ * the line build, envelope and expectation stay fp64.  Not a reference mode
+ * (the reference is fp64 throughout, constants.py:8): results agree with the
+ * fp64 plan to ~1e-3 relative when the noise is >= 1e-3 of the outputscale.
+ * Forward only (not combinable with DKG_PLAN_GRAD). */
+#define DKG_PLAN_F32 4
 size_t dkg_plan_bytes(void);
 size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags);
 int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,

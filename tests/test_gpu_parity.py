@@ -336,3 +336,57 @@ def test_stress_config_parity(target):
     assert acq._plan_for(4).state is not None
     got = acq(X.to(DEV).unsqueeze(-2)).cpu()
     assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
+
+
+# ---------------------------------------------------------------- fp32 contractions (DKG_PLAN_F32)
+# SURVEY.md 8(d) asks for rel 1e-3 against the fp64 build; measured (tools/f32_check.py) the
+# fp32 rounding of Q_X . Q_D (which cancels against s k(x, z) to ~1e-3 of s) moves meaningful KG values by a
+# median 1e-2..1e-1 relative and by up to ~0.8 on the ill-conditioned s = 50 output, so 1e-3 is NOT met;
+# these tests pin the fp32 mode at what it does deliver: every candidate within 5e-2 of the batch's largest
+# KG, and the median relative difference over the meaningful candidates (KG >= 1e-3 max) below 0.2.
+F32_BATCH_TOL = 5e-2
+F32_MEDIAN_REL = 0.2
+
+
+def _f32_vs_f64(workload, target, nX):
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS[workload])
+    Xd = X[:nX].to(DEV).unsqueeze(-2)
+    k64 = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)(Xd).cpu()
+    acq32 = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV, precision="fp32")
+    k32 = acq32(Xd).cpu()
+    assert acq32._plan.f32
+    return k32, k64
+
+
+def _check_f32(k32, k64):
+    d = (k32 - k64).abs()
+    assert bool((d <= F32_BATCH_TOL * k64.abs().max()).all()), f"max |d| {float(d.max()):.3e} vs {float(k64.max()):.3e}"
+    keep = k64.abs() >= 1e-3 * k64.abs().max()
+    rel = (d / k64.abs())[keep]
+    assert float(rel.median()) < F32_MEDIAN_REL, f"median rel {float(rel.median()):.3e}"
+
+
+@pytest.mark.parametrize("target", [None, 0, 2])
+def test_f32_stress_vs_f64(target):
+    """BASELINE.json configs[4] (m=3, n=1024, N=4096, S=32) with fp32 contractions vs the fp64 build."""
+    _check_f32(*_f32_vs_f64("stress32", target, 64))
+
+
+@pytest.mark.parametrize("workload", ["small", "parity6d"])
+def test_f32_small_vs_f64(workload):
+    _check_f32(*_f32_vs_f64(workload, None, 32))
+
+
+def test_f32_refuses_gradient():
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.errors import UnsupportedError
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV, precision="fp32")
+    Xg = X[:4].to(DEV).unsqueeze(-2).requires_grad_(True)
+    with pytest.raises(UnsupportedError):
+        acq(Xg)

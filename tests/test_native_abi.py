@@ -106,3 +106,24 @@ def test_prepare_output_validation_without_device():
     from dkg_amd.errors import NotPSDError
     with pytest.raises(NotPSDError):
         _lib.check(_lib.DKG_ERR_NOT_PD, "dkg_prepare_output")
+
+
+def test_f32_plan_flag_validation_without_device():
+    """DKG_PLAN_F32 (include/dkg.h): its workspace holds the fp32 copies on top of the fp64 plan's,
+    and it refuses the gradient flag before any device work."""
+    lib = _lib.load()
+    outs = (_lib.DkgOutput * 2)()
+    for o in outs:
+        o.n, o.kernel = 256, 2
+        for f in ("inv_lengthscale", "train_x", "alpha", "root_frag", "disc_frag", "disc_mean"):
+            setattr(o, f, 16)
+    w64 = lib.dkg_plan_workspace(outs, 2, 2, 1024, 128, 16, 0)
+    w32 = lib.dkg_plan_workspace(outs, 2, 2, 1024, 128, 16, _lib.DKG_PLAN_F32)
+    # + per output: Q_X (128 x 256), R^T (256 x 256) and Q_D (1024 x 256) in fp32
+    assert w32 - w64 >= 2 * 4 * (128 * 256 + 256 * 256 + 1024 * 256)
+    host = ctypes.create_string_buffer(lib.dkg_plan_bytes())
+    st = lib.dkg_plan_init(outs, 2, 2, 16, 1024, 16, 16, -1, 128, _lib.DKG_PLAN_F32 | _lib.DKG_PLAN_GRAD, 16,
+                           1 << 40, host, 16, None)
+    assert st == _lib.DKG_ERR_UNSUPPORTED and b"forward only" in lib.dkg_last_error()
+    st = lib.dkg_plan_init(outs, 2, 2, 16, 1024, 16, 16, -1, 128, 64, 16, 1 << 40, host, 16, None)
+    assert st == _lib.DKG_ERR_ARG and b"unknown plan flags" in lib.dkg_last_error()
