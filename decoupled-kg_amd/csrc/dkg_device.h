@@ -63,7 +63,16 @@ __device__ __forceinline__ unsigned long long* kst_slot(int dst, const Plan* P, 
 // evaluated for all of them at once.
 constexpr int ENV_CAP = 128;
 constexpr int HCAP = 128;  // GRAD: queued envelope lines per wave before their gradient terms are flushed
-constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lines)  // survivor list per wave (overflow -> walk all lines)
+constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lines)
+// Streaming forward (no LDS staging): the survivor list holds up to
+// LIST_CAP_STREAM entries per wave; a list that does not fit the hull stage
+// (ENV_CAP - 3) is cut down by quickhull rounds (refine_list) instead of the
+// gift wrap over all streamed lines.  VCAP: known hull vertices per wave.
+constexpr int LIST_CAP_STREAM = 512;
+constexpr int VCAP = 64;
+__host__ __device__ constexpr int list_cap(bool refine) { return refine ? LIST_CAP_STREAM : ENV_CAP; }
+// LDS doubles per wave for the refinement's vertex arrays (vb, va, vn)
+constexpr int VREG = 3 * VCAP;
 
 // Gift wrap over all register lines (fallback when the survivor list
 // overflows ENV_CAP): next vertex = argmin of the next intersection, found by
@@ -430,7 +439,7 @@ __device__ __forceinline__ HullGrad envelope_hull_grad(const EnvFilter& f, int l
 // (N + 1 > 64 * 33, or the staging exceeds LDS): every pass rebuilds the
 // lines chunk by chunk (64 * MAXL lines each) through build(c, la, lb);
 // line k = c * 64 * MAXL + lane + 64 t.
-template <int MAXL, bool IDX, class Build>
+template <int MAXL, bool IDX, int CAP = ENV_CAP, class Build>
 __device__ __forceinline__ EnvFilter envelope_filter_stream(int nch, int lane, double* sb, double* sa, int* si,
                                                             Build&& build) {
   EnvFilter f;
@@ -487,7 +496,7 @@ __device__ __forceinline__ EnvFilter envelope_filter_stream(int nch, int lane, d
       if (mk != 0) {
         if (s) {
           const int pos = cnt + lanes_below(mk);
-          if (pos < ENV_CAP) {
+          if (pos < CAP) {
             sb[pos] = bb;
             sa[pos] = a;
             if constexpr (IDX) si[pos] = c * 64 * MAXL + lane + 64 * t;
@@ -555,6 +564,136 @@ __device__ __forceinline__ double envelope_walk_stream(int nch, int nl, int lane
   }
   visit(kc, bc, ac, cL, INFINITY);
   return kg;
+}
+
+// Quickhull refinement of an overflowing survivor list (forward, streaming
+// envelope).  The list holds the cnt <= LIST_CAP_STREAM lines strictly above
+// chord L-T or T-R.  Known hull vertices V (slope order, in vb/va: L, T, R to
+// start) split the slope axis into chords; per chord the entry farthest above
+// it is itself an upper-hull vertex (it maximises a - (chord) at its slope over
+// that interval), so it joins V, and entries not strictly above the new chords
+// are dropped (collinear ones included: the reference walk skips them too,
+// discretekg.py:382-401 takes the larger slope on equal intersections).  Rounds
+// repeat until survivors + new vertices fit the hull stage; the new vertices
+// are then appended to the list (envelope_hull appends L, T, R itself).
+// Heights are h = (a - a_0)(b_1 - b_0) - (b - b_0)(a_1 - a_0), exactly 0 at
+// both chord ends.  Returns the new list length, or -1 (caller walks).
+__device__ __forceinline__ double vchord_h(double b, double a, const double* vb, const double* va, int c) {
+  const double b0 = vb[c], a0 = va[c], b1 = vb[c + 1], a1 = va[c + 1];
+  return (a - a0) * (b1 - b0) - (b - b0) * (a1 - a0);
+}
+
+__device__ __forceinline__ int refine_list(const EnvFilter& f, int cnt, int lane, double* sb, double* sa, double* vb,
+                                        double* va, int* vn) {
+  constexpr int PL = LIST_CAP_STREAM / 64;
+  if (lane == 0) {
+    vb[0] = f.bL; va[0] = f.aL;
+    vb[1] = f.bT; va[1] = f.aT;
+    vb[2] = f.bR; va[2] = f.aR;
+  }
+  int nv = 3, tpos = 1;
+  for (int round = 0; round < 8; ++round) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (cnt + (nv - 3) <= ENV_CAP - 3) break;
+    if (nv >= VCAP / 2 + 1) return -1;  // a round may double the chords
+    double eb[PL], ea[PL], eh[PL];
+    int ec[PL];
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+      const int e = min(lane + 64 * q, max(cnt - 1, 0));
+      eb[q] = sb[e];
+      ea[q] = sa[e];
+      int c = 0;
+      for (int i = 1; i < nv - 1; ++i) c += (eb[q] > vb[i]) ? 1 : 0;
+      ec[q] = c;
+      eh[q] = (lane + 64 * q < cnt) ? vchord_h(eb[q], ea[q], vb, va, c) : -1.0;
+    }
+    // farthest entry above each chord (wave argmax, ties -> lower list index);
+    // its list index goes to vn[chord] (lane 0), -1 when nothing is above
+    int found = 0;
+    uint64_t hasnew = 0;
+    for (int c = 0; c < nv - 1; ++c) {
+      double bh = 0.0;
+      int be = 1 << 30;
+#pragma unroll
+      for (int q = 0; q < PL; ++q) {
+        const bool take = ec[q] == c && eh[q] > bh;
+        bh = take ? eh[q] : bh;
+        be = take ? lane + 64 * q : be;
+      }
+      DKG_BUTTERFLY({
+        const double oh = partner_f64<S_>(bh);
+        const int oe = __shfl_xor(be, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
+        const bool take = oh > bh || (oh == bh && oe < be);
+        bh = take ? oh : bh;
+        be = take ? oe : be;
+      })
+      const int e = __builtin_amdgcn_readfirstlane(be);
+      if (e < cnt) {  // wave-uniform: a line strictly above chord c
+        if (lane == 0) vn[c] = e;
+        hasnew |= 1ull << c;
+        ++found;
+      }
+    }
+    if (found == 0) return -1;  // cnt > 0 entries yet none above a chord: rounding; the caller walks
+    // new vertex set in slope order, built in place from the back by lane 0:
+    // old vertex i moves to i + (new vertices of chords < i); chord i's new
+    // vertex follows it.  Targets are >= sources, so no unread entry is overwritten.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+      for (int i = nv - 1; i >= 0; --i) {
+        const int w = i + __popcll(hasnew & ((1ull << i) - 1));
+        const double b0 = vb[i], a0 = va[i];
+        if (i < nv - 1 && ((hasnew >> i) & 1)) {
+          const int e = vn[i];
+          vb[w + 1] = sb[e];
+          va[w + 1] = sa[e];
+        }
+        vb[w] = b0;
+        va[w] = a0;
+      }
+    }
+    tpos += __popcll(hasnew & ((1ull << tpos) - 1));
+    nv += found;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // re-filter against the new chords and compact in place (entries are in registers)
+    int nc = 0;
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+      int c = 0;
+      for (int i = 1; i < nv - 1; ++i) c += (eb[q] > vb[i]) ? 1 : 0;
+      const bool keep = lane + 64 * q < cnt && vchord_h(eb[q], ea[q], vb, va, c) > 0.0;
+      const uint64_t mk = __ballot(keep);
+      if (keep) {
+        const int pos = nc + lanes_below(mk);
+        sb[pos] = eb[q];
+        sa[pos] = ea[q];
+      }
+      nc += __popcll(mk);
+    }
+    cnt = nc;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (cnt + (nv - 3) > ENV_CAP - 3) return -1;
+  // append the new vertices (every V entry but L, T, R)
+  if (lane == 0) {
+    int pos = cnt;
+    for (int i = 1; i < nv - 1; ++i) {
+      if (i == tpos) continue;
+      sb[pos] = vb[i];
+      sa[pos] = va[i];
+      ++pos;
+    }
+  }
+  return cnt + (nv - 3);
 }
 
 // Whole envelope stage for register-held lines (lines_kg_kernel).
@@ -654,6 +793,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   // k >= 1 reads index k - 1; the pad makes the lane-0 / slot-0 read legal),
   // the weights, then the per-wave survivor lists.
   const int SLp = STREAM ? 0 : stage_stride(N);
+  constexpr int LC = list_cap(STREAM && !GRAD);  // survivor-list capacity per wave
   double* lmu = smem + 2;
   double* lcv = lmu + (size_t)M * SLp;
   double* lw = lcv + (size_t)M * SLp;
@@ -670,7 +810,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   double *sil = nullptr, *shD = nullptr, *suw = nullptr, *sscl = nullptr;
   int* shk = nullptr;
   if constexpr (GRAD) {
-    double* gb = sbuf + (size_t)SW * 2 * ENV_CAP;
+    double* gb = sbuf + (size_t)SW * 2 * LC;
     sidx = reinterpret_cast<int*>(gb);
     qrow = gb + (SW * ENV_CAP + 1) / 2;
     jrow = qrow + (size_t)M * NP;
@@ -758,8 +898,10 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
   if (!GRAD) KST(st, 3);
 
-  double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
-  double* sa = sb + ENV_CAP;
+  double* sb = sbuf + (size_t)wave * 2 * LC;
+  double* sa = sb + LC;
+  // streaming forward: the quickhull refinement's vertex arrays after the lists
+  double* vreg = sbuf + (size_t)SW * 2 * LC + (size_t)wave * VREG;
   double wave_acc = 0.0;
   int* si = nullptr;
   double* gw = nullptr;
@@ -1156,8 +1298,16 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       if (lane == 0)
         for (int dd = 0; dd < d; ++dd) gw[dd] = 0.0;
     } else if constexpr (STREAM) {
-      f = envelope_filter_stream<MAXL, false>(nch, lane, sb, sa, nullptr, build_chunk);
+      f = envelope_filter_stream<MAXL, false, LC>(nch, lane, sb, sa, nullptr, build_chunk);
       if (force_walk && f.status == 0) f.status = 2;
+      if (f.status == 2 && !force_walk && f.cnt <= LC) {
+        // too many survivors for the hull stage: quickhull rounds on the list, not a walk over the lines
+        const int nc = refine_list(f, f.cnt, lane, sb, sa, vreg, vreg + VCAP, reinterpret_cast<int*>(vreg + 2 * VCAP));
+        if (nc >= 0) {
+          f.cnt = nc;
+          f.status = 0;
+        }
+      }
     } else {
       double la[MAXL], lb[MAXL];
       build_lines(la, lb);

@@ -85,7 +85,7 @@ hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStr
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and
 // workgroups per candidate.
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split);
-size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream);
+size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad = false);
 size_t cross_root_lds_bytes(int np, int d);
 
 }  // namespace dkg

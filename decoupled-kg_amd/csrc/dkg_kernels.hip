@@ -473,10 +473,12 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
 
 static int outputs_bucket(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 3 ? 3 : m <= 4 ? 4 : 8; }
 
-size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream) {
+size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad) {
   const int M = outputs_bucket(m);
   const size_t staged = stream ? 0 : 2 * (size_t)M * stage_stride(N);
-  return ((size_t)2 + staged + ((S * m + 1) & ~1) + (size_t)waves * 2 * ENV_CAP) * sizeof(double);
+  const bool refine = stream && !grad;  // streaming forward: long lists + quickhull vertex arrays
+  return ((size_t)2 + staged + ((S * m + 1) & ~1) + (size_t)waves * 2 * list_cap(refine) +
+          (refine ? (size_t)waves * VREG : 0)) * sizeof(double);
 }
 
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream) {
@@ -485,7 +487,7 @@ size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np
                        2 * (size_t)M * DKG_MAX_DIM + (size_t)waves * 64 + DKG_MAX_DIM +
                        (size_t)M * DKG_MAX_DIM + (size_t)waves * (HCAP + max_np + ENV_CAP) +
                        (size_t)(waves * HCAP + 1) / 2;
-  return envelope_lds_bytes(m, N, waves, S, stream) + extra * sizeof(double);
+  return envelope_lds_bytes(m, N, waves, S, stream, true) + extra * sizeof(double);
 }
 
 // ---------------------------------------------------------------------------

@@ -338,6 +338,24 @@ def test_stress_config_parity(target):
     assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
 
 
+@pytest.mark.parametrize("target", [None, 1])
+def test_stress_refinement_parity(target):
+    """Streaming envelope at the stress shape over 24 candidates x 32 scalarisations: ~16 % of the pairs
+    have more chord survivors than the hull stage takes (SURVEY-shaped data, max ~900 of 4097 lines) and go
+    through the quickhull refinement of the survivor list (refine_list) instead of the gift wrap."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS["stress32"])
+    X = X[:24]
+    om = to_oracle(model)
+    ref, _ = discrete_kg_batched(om, X, D, W, target)
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    pairs = acq.forward_pairs(X.to(DEV).unsqueeze(-2)).cpu()
+    got = pairs.mean(-1)
+    assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
+
+
 # ---------------------------------------------------------------- fp32 contractions (DKG_PLAN_F32)
 # SURVEY.md 8(d) asks for rel 1e-3 against the fp64 build; measured (tools/f32_check.py, DESIGN.md 4.6) the
 # fp32 rounding of Q_X . Q_D (which cancels against s k(x, z) to ~1e-3 of s) moves meaningful KG values by a
