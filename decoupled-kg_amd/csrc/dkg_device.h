@@ -583,15 +583,17 @@ __device__ __forceinline__ double vchord_h(double b, double a, const double* vb,
   return (a - a0) * (b1 - b0) - (b - b0) * (a1 - a0);
 }
 
+// nv0 > 0: the vertex set (nv0 entries, T at tpos0) is already in vb/va
+// (refine_stream); otherwise it starts as L, T, R.
 __device__ __forceinline__ int refine_list(const EnvFilter& f, int cnt, int lane, double* sb, double* sa, double* vb,
-                                        double* va, int* vn) {
+                                        double* va, int* vn, int nv0 = 0, int tpos0 = 1) {
   constexpr int PL = LIST_CAP_STREAM / 64;
-  if (lane == 0) {
+  if (nv0 == 0 && lane == 0) {
     vb[0] = f.bL; va[0] = f.aL;
     vb[1] = f.bT; va[1] = f.aT;
     vb[2] = f.bR; va[2] = f.aR;
   }
-  int nv = 3, tpos = 1;
+  int nv = nv0 ? nv0 : 3, tpos = nv0 ? tpos0 : 1;
   for (int round = 0; round < 8; ++round) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -694,6 +696,169 @@ __device__ __forceinline__ int refine_list(const EnvFilter& f, int cnt, int lane
     }
   }
   return cnt + (nv - 3);
+}
+
+// Streaming quickhull round(s) for survivor lists longer than the LDS list
+// holds (cnt > LIST_CAP_STREAM): per chord of the known vertices V (L, T, R to
+// start), one pass over the streamed lines finds the farthest line strictly
+// above it (an upper-hull vertex, as in refine_list); a second pass re-filters
+// the lines against the doubled chord set into the list.  Up to two rounds
+// (3 -> 5 -> 9 vertices), then refine_list continues on the list.  Returns
+// the hull-stage list length, or -1 (the caller walks).
+template <int MAXL, int NV, class Build>
+__device__ __forceinline__ int chord_of(double b, const double (&vb_)[NV], int nv) {
+  int c = 0;
+#pragma unroll
+  for (int i = 1; i < NV - 1; ++i) c += (i < nv - 1 && b > vb_[i]) ? 1 : 0;
+  return c;
+}
+
+template <int NV>
+__device__ __forceinline__ double chord_h_reg(double b, double a, const double (&vb_)[NV], const double (&va_)[NV],
+                                              int c) {
+  double b0 = vb_[0], a0 = va_[0], b1 = vb_[1], a1 = va_[1];
+#pragma unroll
+  for (int i = 1; i < NV - 1; ++i) {
+    const bool s = c == i;
+    b0 = s ? vb_[i] : b0;
+    a0 = s ? va_[i] : a0;
+    b1 = s ? vb_[i + 1] : b1;
+    a1 = s ? va_[i + 1] : a1;
+  }
+  return (a - a0) * (b1 - b0) - (b - b0) * (a1 - a0);
+}
+
+// One streaming round with NV = nv vertices (compile-time bound) read from LDS:
+// new vertices inserted into vb/va (lane 0), survivors of the 2(nv-1) chords
+// written to the list (capacity LIST_CAP_STREAM).  Returns the survivor count
+// (may exceed the capacity), or -1 if no line is above any chord.
+template <int MAXL, int NV, class Build>
+__device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* sb, double* sa, double* vb, double* va,
+                                            int& nv, int& tpos, Build&& build) {
+  constexpr int NC = NV - 1;
+  double vb_[NV], va_[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    vb_[i] = vb[min(i, nv - 1)];
+    va_[i] = va[min(i, nv - 1)];
+  }
+  // pass A: farthest line above each chord (ties -> lowest line index)
+  double bh[NC], bb[NC], ba[NC];
+  int bk[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) { bh[c] = 0.0; bb[c] = 0.0; ba[c] = 0.0; bk[c] = 1 << 30; }
+  for (int ch = 0; ch < nch; ++ch) {
+    double la[MAXL], lb[MAXL];
+    build(ch, la, lb);
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const int k = ch * 64 * MAXL + lane + 64 * t;
+      const int c = chord_of<MAXL, NV, Build>(lb[t], vb_, nv);
+      const double h = chord_h_reg<NV>(lb[t], la[t], vb_, va_, c);
+      const bool live = k < nl;
+#pragma unroll
+      for (int cc = 0; cc < NC; ++cc) {
+        const bool take = live && c == cc && h > bh[cc];
+        bh[cc] = take ? h : bh[cc];
+        bb[cc] = take ? lb[t] : bb[cc];
+        ba[cc] = take ? la[t] : ba[cc];
+        bk[cc] = take ? k : bk[cc];
+      }
+    }
+  }
+  uint64_t hasnew = 0;
+  int found = 0;
+#pragma unroll
+  for (int cc = 0; cc < NC; ++cc) {
+    if (cc >= nv - 1) break;
+    double h = bh[cc], b = bb[cc], a = ba[cc];
+    int k = bk[cc];
+    DKG_BUTTERFLY({
+      const double oh = partner_f64<S_>(h), ob = partner_f64<S_>(b), oa = partner_f64<S_>(a);
+      const int ok = __shfl_xor(k, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
+      const bool take = oh > h || (oh == h && ok < k);
+      h = take ? oh : h;
+      b = take ? ob : b;
+      a = take ? oa : a;
+      k = take ? ok : k;
+    })
+    if (uniform(h > 0.0)) {
+      hasnew |= 1ull << cc;
+      ++found;
+      bb[cc] = b;
+      ba[cc] = a;
+    }
+  }
+  if (found == 0) return -1;
+  // insert the new vertices (lane 0, from the back, as refine_list)
+  if (lane == 0) {
+    for (int i = nv - 1; i >= 0; --i) {
+      const int w = i + __popcll(hasnew & ((1ull << i) - 1));
+      const double b0 = vb[i], a0 = va[i];
+#pragma unroll
+      for (int cc = 0; cc < NC; ++cc)
+        if (cc == i && ((hasnew >> cc) & 1)) {
+          vb[w + 1] = bb[cc];
+          va[w + 1] = ba[cc];
+        }
+      vb[w] = b0;
+      va[w] = a0;
+    }
+  }
+  tpos += __popcll(hasnew & ((1ull << tpos) - 1));
+  nv += found;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // pass B: survivors of the new chords into the list
+  constexpr int NV2 = 2 * NV - 1;
+  double wb_[NV2], wa_[NV2];
+#pragma unroll
+  for (int i = 0; i < NV2; ++i) {
+    wb_[i] = vb[min(i, nv - 1)];
+    wa_[i] = va[min(i, nv - 1)];
+  }
+  int cnt = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    double la[MAXL], lb[MAXL];
+    build(ch, la, lb);
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const int k = ch * 64 * MAXL + lane + 64 * t;
+      const int c = chord_of<MAXL, NV2, Build>(lb[t], wb_, nv);
+      const bool keep = k < nl && chord_h_reg<NV2>(lb[t], la[t], wb_, wa_, c) > 0.0;
+      const uint64_t mk = __ballot(keep);
+      if (mk != 0) {
+        if (keep) {
+          const int pos = cnt + lanes_below(mk);
+          if (pos < LIST_CAP_STREAM) {
+            sb[pos] = lb[t];
+            sa[pos] = la[t];
+          }
+        }
+        cnt += __popcll(mk);
+      }
+    }
+  }
+  return cnt;
+}
+
+template <int MAXL, class Build>
+__device__ __forceinline__ int refine_stream(const EnvFilter& f, int nch, int nl, int lane, double* sb, double* sa,
+                                             double* vb, double* va, int* vn, Build&& build) {
+  if (lane == 0) {
+    vb[0] = f.bL; va[0] = f.aL;
+    vb[1] = f.bT; va[1] = f.aT;
+    vb[2] = f.bR; va[2] = f.aR;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int nv = 3, tpos = 1;
+  int cnt = stream_round<MAXL, 3>(nch, nl, lane, sb, sa, vb, va, nv, tpos, build);
+  if (cnt > LIST_CAP_STREAM) cnt = stream_round<MAXL, 5>(nch, nl, lane, sb, sa, vb, va, nv, tpos, build);
+  if (cnt < 0 || cnt > LIST_CAP_STREAM) return -1;
+  return refine_list(f, cnt, lane, sb, sa, vb, va, vn, nv, tpos);
 }
 
 // Whole envelope stage for register-held lines (lines_kg_kernel).
@@ -1300,9 +1465,13 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     } else if constexpr (STREAM) {
       f = envelope_filter_stream<MAXL, false, LC>(nch, lane, sb, sa, nullptr, build_chunk);
       if (force_walk && f.status == 0) f.status = 2;
-      if (f.status == 2 && !force_walk && f.cnt <= LC) {
-        // too many survivors for the hull stage: quickhull rounds on the list, not a walk over the lines
-        const int nc = refine_list(f, f.cnt, lane, sb, sa, vreg, vreg + VCAP, reinterpret_cast<int*>(vreg + 2 * VCAP));
+      if (f.status == 2 && !force_walk) {
+        // too many survivors for the hull stage: quickhull rounds (on the streamed lines while the
+        // list overflows its LDS capacity, then on the list), not a walk over the lines per vertex
+        int* vn = reinterpret_cast<int*>(vreg + 2 * VCAP);
+        const int nc = (f.cnt <= LC) ? refine_list(f, f.cnt, lane, sb, sa, vreg, vreg + VCAP, vn)
+                                     : refine_stream<MAXL>(f, nch, NL, lane, sb, sa, vreg, vreg + VCAP, vn,
+                                                           build_chunk);
         if (nc >= 0) {
           f.cnt = nc;
           f.status = 0;
