@@ -443,42 +443,46 @@ template <int MAXL, bool IDX, int CAP = ENV_CAP, class Build>
 __device__ __forceinline__ EnvFilter envelope_filter_stream(int nch, int lane, double* sb, double* sa, int* si,
                                                             Build&& build) {
   EnvFilter f;
-  double bmin = INFINITY, bmax = -INFINITY, amax = -INFINITY;
+  // One pass for the extremes with their exact ties (lexicographic: L = min b
+  // then max a, R = max b then max a, T = max a then min b): the streamed
+  // lines cost loads, so this trades select work for a whole pass over them.
+  double bmin = INFINITY, aLx = -INFINITY, bmax = -INFINITY, aRx = -INFINITY, amax = -INFINITY, bTx = INFINITY;
   for (int c = 0; c < nch; ++c) {
     double la[MAXL], lb[MAXL];
     build(c, la, lb);
 #pragma unroll
     for (int t = 0; t < MAXL; ++t) {
-      bmin = fmin(bmin, lb[t]);
-      bmax = fmax(bmax, lb[t]);
-      amax = fmax(amax, la[t]);
+      const double a = la[t], b = lb[t];
+      const bool l = b < bmin || (b == bmin && a > aLx);
+      bmin = l ? b : bmin;
+      aLx = l ? a : aLx;
+      const bool r = b > bmax || (b == bmax && a > aRx);
+      bmax = r ? b : bmax;
+      aRx = r ? a : aRx;
+      const bool tt = a > amax || (a == amax && b < bTx);
+      amax = tt ? a : amax;
+      bTx = tt ? b : bTx;
     }
   }
   DKG_BUTTERFLY({
-    bmin = fmin(bmin, partner_f64<S_>(bmin));
-    bmax = fmax(bmax, partner_f64<S_>(bmax));
-    amax = fmax(amax, partner_f64<S_>(amax));
+    const double ob = partner_f64<S_>(bmin), oa = partner_f64<S_>(aLx);
+    const bool l = ob < bmin || (ob == bmin && oa > aLx);
+    bmin = l ? ob : bmin;
+    aLx = l ? oa : aLx;
+    const double ob2 = partner_f64<S_>(bmax), oa2 = partner_f64<S_>(aRx);
+    const bool r = ob2 > bmax || (ob2 == bmax && oa2 > aRx);
+    bmax = r ? ob2 : bmax;
+    aRx = r ? oa2 : aRx;
+    const double oa3 = partner_f64<S_>(amax), ob3 = partner_f64<S_>(bTx);
+    const bool tt = oa3 > amax || (oa3 == amax && ob3 < bTx);
+    amax = tt ? oa3 : amax;
+    bTx = tt ? ob3 : bTx;
   })
   if (!uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax)) {
     f.status = 1;
     return f;
   }
-  double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
-  for (int c = 0; c < nch; ++c) {
-    double la[MAXL], lb[MAXL];
-    build(c, la, lb);
-#pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      aL = fmax(aL, (lb[t] == bmin) ? la[t] : -INFINITY);
-      aR = fmax(aR, (lb[t] == bmax) ? la[t] : -INFINITY);
-      bT = fmin(bT, (la[t] == amax) ? lb[t] : INFINITY);
-    }
-  }
-  DKG_BUTTERFLY({
-    aL = fmax(aL, partner_f64<S_>(aL));
-    aR = fmax(aR, partner_f64<S_>(aR));
-    bT = fmin(bT, partner_f64<S_>(bT));
-  })
+  const double aL = aLx, aR = aRx, bT = bTx;
   const double bL = bmin, bR = bmax, aT = amax;
   f.bL = bL; f.aL = aL; f.bR = bR; f.aR = aR; f.bT = bT; f.aT = aT;
   const double db1 = bT - bL, da1 = aT - aL, k1 = aL * db1 - bL * da1;
