@@ -137,43 +137,18 @@ def main():
     plan = acq._plan_for(w.B)
     Xd = X.to(dev).contiguous()
     E = max(1, min(args.exchange_every, args.steps))
-    kbufs = [torch.empty(E, w.B, dtype=torch.double, device=dev) for _ in range(2)]
-    gathered = [torch.empty(world * E * w.B, dtype=torch.double, device=dev) for _ in range(2)]
-    works = [None, None]
-
-    def exchange(slot, rows):
-        """One async RCCL collective over the first ``rows`` forward batches held in ``kbufs[slot]``."""
-        blk = kbufs[slot][:rows].view(-1)
-        if args.shard == "candidates":
-            works[slot] = dist.all_gather_into_tensor(gathered[slot][:world * rows * w.B], blk, async_op=True)
-        else:
-            blk.mul_(w.S)           # partial sums over this rank's rows; / (S*world) after the reduce
-            works[slot] = dist.all_reduce(blk, op=dist.ReduceOp.SUM, async_op=True)
+    from dkg_amd.dist import BatchExchange
+    xchg = BatchExchange(w.B, E, "gather" if args.shard == "candidates" else "reduce", S_local=w.S, device=dev)
 
     def step(k):
-        slot, row = (k // E) % 2, k % E
-        if world > 1 and row == 0 and works[slot] is not None:
-            works[slot].wait()      # the exchange that last used this buffer is done
-            works[slot] = None
-        kg = kbufs[slot][row]
+        kg = xchg.row(k)
         plan.forward_into(Xd, kg)
-        if world > 1 and row == E - 1:
-            exchange(slot, E)
+        xchg.done(k)
         return kg
-
-    def flush(nsteps):
-        """Exchange the rows of a final, partially filled buffer."""
-        rem = nsteps % E
-        if world > 1 and rem:
-            exchange((nsteps // E) % 2, rem)
 
     for k in range(args.warmup):
         step(k)
-    flush(args.warmup)
-    for i, wk in enumerate(works):
-        if wk is not None:
-            wk.wait()
-            works[i] = None
+    xchg.flush(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -183,10 +158,7 @@ def main():
     ev0.record()
     for k in range(args.steps):
         step(k)
-    flush(args.steps)
-    for wk in works:
-        if wk is not None:
-            wk.wait()
+    xchg.flush(args.steps)
     ev1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0

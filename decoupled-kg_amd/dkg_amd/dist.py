@@ -115,3 +115,85 @@ class ShardedDiscreteKG:
         return out.to(X.device).reshape(batch_shape)
 
     __call__ = forward
+
+
+class BatchExchange:
+    """K forward batches per collective ("loop K forward batches per all-reduce,
+    count = K*B"): the throughput driver's exchange of per-candidate KG values.
+
+    Step k writes its ``B`` values into ``row(k)`` (row k % K of one of two [K, B] buffers);
+    after the K-th row of a buffer ``done(k)`` starts one async collective over the whole
+    buffer, and the next K steps fill the other buffer while it runs.  A buffer is only reused
+    after its collective has completed.  ``mode="gather"`` (candidates sharded): an all-gather,
+    every rank ends with [world, rows, B].  ``mode="reduce"`` (scalarisations sharded): the rows
+    hold per-rank means over ``S_local`` rows; they are scaled to partial sums and all-reduced
+    (the caller divides by the total S).  ``sink`` (tests): completed results are appended to it.
+    """
+
+    def __init__(self, B: int, every: int, mode: str = "gather", S_local: int = 1, device=None,
+                 dtype=torch.double, sink: Optional[list] = None):
+        if mode not in ("gather", "reduce"):
+            raise ValueError(f"mode must be 'gather' or 'reduce', got {mode!r}")
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.B, self.E, self.mode, self.S_local = int(B), max(1, int(every)), mode, S_local
+        self.bufs = [torch.zeros(self.E, self.B, dtype=dtype, device=device) for _ in range(2)]
+        self.gathered = [torch.zeros(self.world * self.E * self.B, dtype=dtype, device=device) for _ in range(2)]
+        self.works = [None, None]
+        self.rows = [0, 0]
+        self.sink = sink
+
+    def _slot(self, k: int):
+        return (k // self.E) % 2, k % self.E
+
+    def _finish(self, slot: int) -> None:
+        if self.works[slot] is not None:
+            self.works[slot].wait()
+            self.works[slot] = None
+            if self.sink is not None:
+                r = self.rows[slot]
+                if self.mode == "gather":
+                    self.sink.append(self.gathered[slot][:self.world * r * self.B].view(self.world, r, self.B).clone())
+                else:
+                    self.sink.append(self.bufs[slot][:r].clone())
+
+    def row(self, k: int) -> Tensor:
+        """The [B] buffer step k writes (waits for the collective that last used its buffer)."""
+        slot, r = self._slot(k)
+        if r == 0:
+            self._finish(slot)
+        return self.bufs[slot][r]
+
+    def _exchange(self, slot: int, rows: int) -> None:
+        self.rows[slot] = rows
+        if self.world == 1:
+            if self.mode == "gather":
+                self.gathered[slot][:rows * self.B].copy_(self.bufs[slot][:rows].reshape(-1))
+            self.works[slot] = _Done()
+            return
+        blk = self.bufs[slot][:rows].view(-1)
+        if self.mode == "gather":
+            self.works[slot] = dist.all_gather_into_tensor(self.gathered[slot][:self.world * rows * self.B], blk,
+                                                           async_op=True)
+        else:
+            blk.mul_(self.S_local)
+            self.works[slot] = dist.all_reduce(blk, op=dist.ReduceOp.SUM, async_op=True)
+
+    def done(self, k: int) -> None:
+        """Step k has written its row: exchange the buffer if it is full."""
+        slot, r = self._slot(k)
+        if r == self.E - 1:
+            self._exchange(slot, self.E)
+
+    def flush(self, nsteps: int) -> None:
+        """After ``nsteps`` steps: exchange a partially filled last buffer, then wait for everything."""
+        rem = nsteps % self.E
+        if rem:
+            self._exchange((nsteps // self.E) % 2, rem)
+        last = ((nsteps - 1) // self.E) % 2 if nsteps > 0 else 1
+        for slot in (1 - last, last):  # the older buffer's collective first
+            self._finish(slot)
+
+
+class _Done:
+    def wait(self):
+        return None

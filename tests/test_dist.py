@@ -68,3 +68,20 @@ def test_sharded_matches_unsharded(tmp_path, axis, B, S, target):
         assert sum(c[0][1] for c in calls if c) == S and all(c[0][0] == B for c in calls if c)
     else:
         assert sum(c[0][0] for c in calls if c) == B and all(c[0][1] == S for c in calls if c)
+
+
+@pytest.mark.parametrize("mode,steps,every", [("gather", 7, 3), ("gather", 6, 3), ("reduce", 7, 3),
+                                              ("reduce", 2, 64)])
+def test_batch_exchange(tmp_path, mode, steps, every):
+    """bench.py's K-batches-per-collective exchange (dkg_amd.dist.BatchExchange) over 2 gloo ranks:
+    every step's values arrive, in order, in exactly ceil(steps / K) collectives, including a
+    partially filled last buffer and double-buffer reuse across a warm-up and a timed pass."""
+    out = str(tmp_path / f"xchg_{mode}_{steps}_{every}.pt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "exchange_worker.py"),
+           mode, str(steps), str(every), out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = torch.load(out, weights_only=True)
+    assert res["n"] == -(-steps // every)
+    assert torch.equal(res["got"], res["exp"])
