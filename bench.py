@@ -76,6 +76,15 @@ def stage_model(w, m, n, N, B, S, d):
             "envelope_kernel": (fl_env, by_env)}
 
 
+def survey_model(m, n, N, S, B, d):
+    """SURVEY.md 8(d) / BASELINE.md algorithmic cost of one forward of B candidates (fp64):
+    F = B * (sum_i [2 n_i^2 + 2 n_i N + (3d+8)(n_i+N+1)] + S (N+1)(5m+1)),
+    Bytes = 8 [sum_i (n_i^2 + n_i N + N + n_i d) + N d + B d + S m + B]."""
+    f_eval = sum(2 * nn * nn + 2 * nn * N + (3 * d + 8) * (nn + N + 1) for nn in n) + S * (N + 1) * (5 * m + 1)
+    by = 8 * (sum(nn * nn + nn * N + N + nn * d for nn in n) + N * d + B * d + S * m + B)
+    return f_eval * B, by
+
+
 def cpu_baseline(model, D, W, X, target, seconds, threads):
     """The oracle's structure-faithful restatement of the reference path on host cores."""
     from oracle.discretekg import calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output
@@ -192,6 +201,24 @@ def main():
             "avg_launch_us": avg_ms[dom] * 1e3,
             "stages_us": {n: a * 1e3 for n, a in zip(names, avg_ms)}}
 
+    # ---- whole-forward roofline as BASELINE.md defines it: max(F/P, Bytes/BW) / T_measured
+    f_fwd, b_fwd = survey_model(w.m, [mm.num_train for mm in model.models], D.shape[0], w.S, w.B, w.d)
+    t_fwd = elapsed / args.steps
+    t_min = max(f_fwd / (FP64_PEAK_TFLOPS * 1e12), b_fwd / (HBM_PEAK_GBS * 1e9))
+    fwd_roof = {"definition": "BASELINE.md: max(F/P_fp64, Bytes/BW_HBM) / T_forward", "flops": f_fwd,
+                "bytes": b_fwd, "t_min_us": t_min * 1e6, "t_forward_us": t_fwd * 1e6, "frac": t_min / t_fwd}
+
+    # ---- SURVEY.md 8(d) diagnostics of the batch: short-circuit rate, KG distribution, envelope sizes
+    kg_s, pairs_s, hull_s = plan.forward_stats(Xd)
+    pairs_c, hull_c, kg_c = pairs_s.cpu(), hull_s.cpu().long(), kg_s.cpu()
+    hist = torch.bincount(hull_c.reshape(-1)).tolist()
+    pair_stats = {"pairs": int(pairs_c.numel()),
+                  "short_circuit_frac": float((hull_c == 1).double().mean()),
+                  "zero_kg_frac": float((pairs_c == 0).double().mean()),
+                  "envelope_lines_mean": float(hull_c.double().mean()),
+                  "envelope_lines_hist": {str(h): c for h, c in enumerate(hist) if c},
+                  "kg_quantiles": {str(q): float(torch.quantile(kg_c, q)) for q in (0.0, 0.1, 0.5, 0.9, 1.0)}}
+
     # ---- value + gradient (dkg_plan_forward_grad: the optimize_acqf L-BFGS-B path), same batch
     grad_info = None
     if args.grad_steps > 0 and args.precision == "fp64":
@@ -236,6 +263,8 @@ def main():
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
             "roofline": roof,
+            "forward_roofline": fwd_roof,
+            "batch_stats": pair_stats,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

@@ -46,6 +46,7 @@ struct WsLayout {
   size_t mux_all, var_all, cov_all, mu_all;
   size_t wg_part;
   size_t tickets;
+  size_t hull_pairs;
   size_t total;
 };
 
@@ -98,6 +99,8 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
   off = align256(off + (size_t)std::max(B, 1) * split * sizeof(double));
   L.tickets = off;
   off = align256(off + Bp * sizeof(int));
+  L.hull_pairs = off;
+  off = align256(off + (size_t)std::max(B, 1) * std::max(S, 1) * sizeof(int));
   L.total = off;
   return L;
 }
@@ -195,6 +198,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->cov_stride = (int64_t)std::max(max_B, 1) * std::max(N, 1);
   P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
+  P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
   static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
   static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
   P->debug_env = (denv ? std::atoi(denv) : 0) | ((flags & DKG_PLAN_FORCE_WALK) ? 1 : 0);
@@ -451,6 +455,15 @@ int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const dou
   if (!xnew || !kg || !dkg_dx) return fail(DKG_ERR_ARG, "NULL data pointer");
   return hip_check(launch_forward_grad(h, static_cast<const Plan*>(dev_plan), xnew, B, kg, dkg_dx,
                                        (hipStream_t)stream), "forward_grad");
+}
+
+int dkg_plan_hull_sizes(const void* host_plan, int* out, int B, void* stream) {
+  if (!host_plan || !out) return fail(DKG_ERR_ARG, "NULL pointer");
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  if (B < 0 || B > h.max_B) return fail(DKG_ERR_ARG, "B=%d outside [0, %d]", B, h.max_B);
+  if (B == 0) return DKG_OK;
+  return hip_check(hipMemcpyAsync(out, h.hull_pairs, sizeof(int) * (size_t)B * h.S, hipMemcpyDeviceToDevice,
+                                  (hipStream_t)stream), "hipMemcpyAsync(hull sizes)");
 }
 
 int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,

@@ -1046,24 +1046,34 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       sil[i * DKG_MAX_DIM + dd] = P->o[i].inv_lengthscale[dd];
     }
   }
+  // Padding lines k = N+1 .. 64*MAXL-1 (read at indices N .. 64*MAXL-2) come
+  // out of the branch-free line build as (a = NaN, b = b_0): mu = NaN makes
+  // the intercept NaN whatever the weights, and cov = the candidate's own
+  // variance gives line 0's slope bit for bit (same FMAs, same order).  NaN
+  // drops out of every fmin/fmax (maxNum) and fails every comparison, so the
+  // padding lines are never an extreme, a tie, a survivor or counted, and
+  // the register lines need no per-slot padding selects.  Indices the DMA
+  // does not touch (>= stage_len(N)) are written while it is in flight; the
+  // ones it over-writes with its last piece (N .. stage_len(N)-1, only when N
+  // is not a multiple of 128) after it has landed.
+  const int SLd = STREAM ? 0 : stage_len(N);
+  auto pad_lines = [&](int lo, int hi) {
+    const int np_ = hi - lo;
+    for (int e = threadIdx.x; e < m * np_; e += blockDim.x) {
+      const int i = e / np_, idx = lo + e % np_;
+      lmu[(size_t)i * SLp + idx] = __builtin_nan("");
+      if (full || i == target) lcv[(size_t)i * SLp + idx] = var_all[(size_t)i * bpad + b];
+    }
+  };
+  if constexpr (!STREAM) pad_lines(max(N, SLd), 64 * MAXL - 1);
   if (!GRAD) KST(st, 2);  // GRAD stamps: 2 preamble done, 3 filter, 4 hull, 5 gradient flush (first pair)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (!STREAM) {
-    // Padding lines k = N+1 .. 64*MAXL-1 (read at indices N .. 64*MAXL-2) come
-    // out of the branch-free line build as (a = NaN, b = b_0): mu = NaN makes
-    // the intercept NaN whatever the weights, and cov = the candidate's own
-    // variance gives line 0's slope bit for bit (same FMAs, same order).  NaN
-    // drops out of every fmin/fmax (maxNum) and fails every comparison, so the
-    // padding lines are never an extreme, a tie, a survivor or counted, and
-    // the register lines need no per-slot padding selects.
-    const int npad = 64 * MAXL - 1 - N;
-    for (int e = threadIdx.x; e < m * npad; e += blockDim.x) {
-      const int i = e / npad, idx = N + e % npad;
-      lmu[(size_t)i * SLp + idx] = __builtin_nan("");
-      if (full || i == target) lcv[(size_t)i * SLp + idx] = s_pp[i * 6 + 4];
+    if (SLd > N) {  // uniform
+      pad_lines(N, min(SLd, 64 * MAXL - 1));
+      __syncthreads();
     }
-    __syncthreads();
   }
   if (!GRAD) KST(st, 3);
 
@@ -1166,7 +1176,6 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       }
     };
     const int nch = (NL + 64 * MAXL - 1) / (64 * MAXL);
-    auto noop_visit = [](int, double, double, double, double) {};
     auto build_lines = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
       const double* mup[M];
 #pragma unroll
@@ -1214,6 +1223,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     };
 
     double kgj;
+    int hn = 1;  // upper-envelope lines of this pair (recorded with kg_pairs)
     EnvFilter f;
     if constexpr (GRAD) {
       if constexpr (STREAM) {
@@ -1491,15 +1501,20 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     } else if (f.status == 1) {
       kgj = 0.0;
     } else if (f.status == 0) {
-      kgj = envelope_hull(f, lane, sb, sa, nullptr);
+      kgj = envelope_hull(f, lane, sb, sa, &hn);
     } else if constexpr (STREAM) {  // list overflow: gift wrap over the streamed lines
-      kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, noop_visit, -1);
+      auto count_visit = [&](int, double, double, double, double) { ++hn; };
+      hn = 0;
+      kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, count_visit, -1);
     } else {  // list overflow: gift wrap over the (rebuilt) register lines
       double la[MAXL], lb[MAXL];
       build_lines(la, lb);
-      kgj = envelope_walk<MAXL>(la, lb, NL, lane, f.bL, f.aL, f.bR, f.bT, nullptr);
+      kgj = envelope_walk<MAXL>(la, lb, NL, lane, f.bL, f.aL, f.bR, f.bT, &hn);
     }
-    if (pairs_out != nullptr && lane == 0) pairs_out[(size_t)b * S + j] = kgj;
+    if (pairs_out != nullptr && lane == 0) {
+      pairs_out[(size_t)b * S + j] = kgj;
+      if constexpr (!GRAD) P->hull_pairs[(size_t)b * S + j] = hn;
+    }
     wave_acc += kgj;
   }
 

@@ -41,6 +41,7 @@ struct Plan {
   float* q32[DKG_MAX_OUTPUTS];      // F32: quad-packed K(x, X) R per output (workspace)
   float* root32[DKG_MAX_OUTPUTS];   // F32: quad-packed R^T (fp32 copy of root_frag, plan init)
   float* disc32[DKG_MAX_OUTPUTS];   // F32: quad-packed Q_D (fp32 copy of disc_frag, plan init)
+  int* hull_pairs;                  // [max_B x S] upper-envelope lines per pair (written with kg_pairs)
 };
 
 // By-value arguments of the state-preparation use of the cross stage.

@@ -74,6 +74,7 @@ SIGNATURES = {
                                        POINTER(c_float)]),
     "dkg_plan_time_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                     c_int, POINTER(c_float)]),
+    "dkg_plan_hull_sizes": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "dkg_lines_kg": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_debug_read_kstamps": (c_int, [c_void_p, c_int]),
     "dkg_debug_wave_ops": (c_int, [c_void_p, c_void_p, c_void_p]),

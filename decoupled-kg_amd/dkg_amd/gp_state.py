@@ -179,6 +179,21 @@ class ForwardPlan:
         if st:
             _lib.check(st, "dkg_plan_forward")
 
+    def forward_stats(self, X: torch.Tensor):
+        """One forward with diagnostics: KG [B], KG per (candidate, scalarisation) [B, S] and the number
+        of upper-envelope lines per pair [B, S] (int32; 1 = short-circuit), all on the device."""
+        X = X.detach().to(self.device, torch.double).contiguous()
+        B = X.shape[0]
+        if B > self.max_B:
+            raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
+        kg = torch.empty(B, dtype=torch.double, device=self.device)
+        pairs = torch.empty(B, self.S, dtype=torch.double, device=self.device)
+        hull = torch.empty(B, self.S, dtype=torch.int32, device=self.device)
+        self.forward_into(X, kg, pairs)
+        _lib.check(_lib.load().dkg_plan_hull_sizes(self.host, _lib.ptr(hull), B, current_stream_ptr(self.device)),
+                   "dkg_plan_hull_sizes")
+        return kg, pairs, hull
+
     def forward_grad(self, X: torch.Tensor):
         """KG[B] and dKG/dx [B, d] for candidates X (B x d): one C call."""
         if not self.grad:

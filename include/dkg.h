@@ -194,6 +194,12 @@ int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const do
  * where only the candidate's own line 0 intercept and the slopes depend on x. */
 int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                           double* dkg_dx, void* stream);
+/* Envelope sizes of the plan's last forward that was given kg_pairs (same B):
+ * out[b*S + j] = the number of upper-envelope lines of pair (b, j), i.e. the
+ * len(indices) of calculate_epigraph_indices (discretekg.py:341-412); 1 when the
+ * pair short-circuits (all |b| < 1e-9, :363-367).  Device int[B x S]; stream
+ * ordered.  Diagnostics (log the envelope-size histogram). */
+int dkg_plan_hull_sizes(const void* host_plan, int* out, int B, void* stream);
 /* Benchmark helper: average HIP-event duration (ms) of `reps` back-to-back
  * launches of one stage (0 cross_root, 1 posterior_cov, 2 envelope) on
  * `stream`, after one full forward that primes its inputs; a final full

@@ -408,3 +408,27 @@ def test_f32_refuses_gradient():
     Xg = X[:4].to(DEV).unsqueeze(-2).requires_grad_(True)
     with pytest.raises(UnsupportedError):
         acq(Xg)
+
+
+# ---------------------------------------------------------------- envelope sizes (dkg_plan_hull_sizes)
+@pytest.mark.parametrize("workload,nX", [("small", 8), ("parity6d", 8), ("stress32", 4)])
+def test_envelope_sizes_match_reference_walk(workload, nX):
+    """The number of upper-envelope lines per (candidate, scalarisation) that the envelope stage reports
+    (register hull, quickhull-refined lists and the streamed walk alike) equals len(indices) of the
+    reference walk (calculate_epigraph_indices, discretekg.py:341-412) on the oracle's lines."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+    from oracle.discretekg import calculate_epigraph_indices, lines_batched
+
+    model, D, X, W = make_problem(WORKLOADS[workload])
+    X = X[:nX]
+    a, b = lines_batched(to_oracle(model), X, D, W, None)
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    kg, pairs, hull = acq._plan_for(nX).forward_stats(X.to(DEV))
+    ref = torch.tensor([[len(calculate_epigraph_indices(a[i, j], b[i, j])[0]) for j in range(W.shape[0])]
+                        for i in range(nX)])
+    got = hull.cpu().long()
+    agree = float((got == ref).double().mean())
+    # near-collinear vertices may be classified differently under the two roundings of the lines
+    assert agree >= 0.95 and int((got - ref).abs().max()) <= 2, f"agree {agree:.3f}, ref {ref.tolist()}, got {got.tolist()}"
+    torch.testing.assert_close(pairs.mean(-1), kg, rtol=1e-12, atol=1e-300)

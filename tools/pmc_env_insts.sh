@@ -5,7 +5,7 @@ set -uo pipefail
 out=gpurun_out/${1:-pmcins}
 mkdir -p "$out"
 export TMPDIR=/tmp
-B="python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 --profile-reps 1"
+B="python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 --profile-reps 1 --grad-steps 0"
 for f in 0; do
   DKG_DEBUG_ENV_FLAGS=$f timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH --output-format csv -d "$out/a$f" -o run -- $B > /dev/null 2>&1 || exit 1
   DKG_DEBUG_ENV_FLAGS=$f timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --output-format csv -d "$out/b$f" -o run -- $B > /dev/null 2>&1 || exit 1
