@@ -1,0 +1,120 @@
+"""Multi-objective BO loop over the device KG: the reference's ``SMOKE_TEST`` pipeline path
+without BoTorch (BASELINE.json configs[0]).
+
+What it restates (reference files, read for behaviour only):
+
+* ``pipeline/main.py:171-216`` ``run_pipeline``: 6 initial Sobol points, then ``run_mobo`` twice,
+  once with separate (decoupled) objective evaluations and costs ``[1, 10]``, once with full
+  evaluations; ``max_n_batch = 2`` under ``SMOKE_TEST``;
+* ``pipeline/nodes/bo_loop.py:48-59`` ``generate_initial_data`` (Sobol in the bounds, every
+  objective evaluated at every point);
+* ``:122-131`` the ``discrete_kg`` spec under ``SMOKE_TEST``: 3 grid points per axis, 2 restarts,
+  4 raw samples, ``batch_limit = 1``, ``max_iter = 200``;
+* ``run_mobo``'s query step (``:380-450``): decoupled, the spec's ``optimize_for_single_objective``
+  picks (x, objective) by KG per cost and only that objective is evaluated and appended to its own
+  training set; full, ``optimize_for_full_evaluation`` picks x and every objective is evaluated;
+* ``modules/gp_testproblem.py:76-98``: the objective of a ``gp-sample`` problem is the posterior
+  mean of the problem GP, evaluated here on the device (``dkg_prepare_output`` + ``dkg_cross_root``);
+* the ``fit_hyperparams = never`` model path (``bo_loop.py:574-619``): the problem's fixed
+  hyperparameters, noise at the 1e-8 floor.  Hyperparameter fitting (``fit_gpytorch_mll``) is not
+  restated: it is outside the KG path.
+
+Scalarisation weights are drawn per step with the reference's qMC simplex sampler
+(``bo_loop.py:84-118``, ``dkg_amd.utils.sample_simplex``).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+from torch import Tensor
+
+from .gp_state import DeviceGPState
+from .model import ModelListGPState, SingleTaskGPState
+from .optim import DiscreteKgOptimisationSpec, draw_sobol_samples
+from .utils import sample_simplex
+
+NEVER_FIT_NOISE = 1e-8  # bo_loop.py:583-588
+
+
+class GPProblem:
+    """A ``gp-sample`` test problem: objective i at x is the posterior mean of output i of a fixed GP
+    (``gp_testproblem.py:76-98``), computed by the library's kernels on ``device``."""
+
+    def __init__(self, gp: ModelListGPState, bounds: Optional[Tensor] = None, device=None):
+        self.gp = gp
+        d = gp.input_dim
+        self.bounds = (torch.stack([torch.zeros(d), torch.ones(d)]) if bounds is None
+                       else torch.as_tensor(bounds, dtype=torch.double).reshape(2, d))
+        self.device = device
+        self.num_objectives = gp.num_outputs
+        self.evaluations = 0
+
+    def __call__(self, X: Tensor) -> Tensor:
+        """[n, d] -> [n, m] objective values (model-space posterior means, then any Standardize)."""
+        X = torch.as_tensor(X, dtype=torch.double).reshape(-1, self.gp.input_dim)
+        st = DeviceGPState(self.gp, X, self.device)
+        n = X.shape[0]
+        out = torch.stack([c.disc_mean[:n] * c.state.y_std + c.state.y_mean for c in st.outputs], dim=-1)
+        self.evaluations += n
+        return out.cpu()
+
+
+def surrogate(train_x: Sequence[Tensor], train_y: Sequence[Tensor], hyper: Dict[str, Sequence[float]],
+              noise: float = NEVER_FIT_NOISE) -> ModelListGPState:
+    """The BO model on the observations so far, one output per objective with its own data
+    (decoupled evaluations give every objective its own training set), fixed hyperparameters."""
+    outs = [SingleTaskGPState(train_x[i], train_y[i], torch.tensor(hyper["length_scales"][i]),
+                              float(hyper["output_scales"][i]), noise, float(hyper["means"][i]))
+            for i in range(len(train_x))]
+    return ModelListGPState(*outs)
+
+
+def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bool, n_iter: int = 2,
+             n_init: int = 6, costs: Sequence[float] = (1, 10), n_scalarisations: int = 16,
+             spec: Optional[DiscreteKgOptimisationSpec] = None, seed: int = 0) -> Dict[str, List]:
+    """``bo_loop.run_mobo`` with the discrete-KG strategy for ``n_iter`` BO steps; returns the
+    query history (x, objective index or None for full evaluation, observed values, acquisition)."""
+    m, d = problem.num_objectives, problem.gp.input_dim
+    torch.manual_seed(seed)  # the pipeline's --seed (cli.py): initialize_q_batch's Boltzmann draw
+    spec = spec or DiscreteKgOptimisationSpec(n_discretisation_points_per_axis=3, num_restarts=2, raw_samples=4,
+                                              batch_limit=1, max_iter=200, device=problem.device, seed=seed)
+    x0 = draw_sobol_samples(problem.bounds, n_init, 1, seed=seed).squeeze(-2)
+    y0 = problem(x0)
+    train_x = [x0.clone() for _ in range(m)]
+    train_y = [y0[:, i].clone() for i in range(m)]
+    hist: Dict[str, List] = {"x": [], "obj_index": [], "obj": [], "acq": [], "cost": []}
+    for it in range(n_iter):
+        W = sample_simplex(m, n_scalarisations, qmc=True, seed=seed + 1 + it, dtype=torch.double)
+        model = surrogate(train_x, train_y, hyper)
+        if separate:
+            x, i, acq = spec.optimize_for_single_objective(model, costs, d, scalarisation_weights=W)
+            x = x.reshape(1, d).cpu()
+            y = problem(x)[0]
+            train_x[i] = torch.cat([train_x[i], x])
+            train_y[i] = torch.cat([train_y[i], y[i:i + 1]])
+            hist["obj_index"].append(int(i))
+            hist["obj"].append(float(y[i]))
+            hist["cost"].append(float(costs[i]))
+        else:
+            x, acq = spec.optimize_for_full_evaluation(model, d, scalarisation_weights=W)
+            x = x.reshape(1, d).cpu()
+            y = problem(x)[0]
+            for i in range(m):
+                train_x[i] = torch.cat([train_x[i], x])
+                train_y[i] = torch.cat([train_y[i], y[i:i + 1]])
+            hist["obj_index"].append(None)
+            hist["obj"].append(y.tolist())
+            hist["cost"].append(float(sum(costs)))
+        hist["x"].append(x[0].tolist())
+        hist["acq"].append(float(acq))
+    hist["n_observations"] = [int(t.shape[0]) for t in train_x]
+    return hist
+
+
+def run_smoke(problem: GPProblem, hyper: Dict[str, Sequence[float]], seed: int = 0) -> Dict[str, Dict]:
+    """``run_pipeline`` under ``SMOKE_TEST`` (``main.py:171-216``): the separate-evaluation run and
+    the full-evaluation run, two BO steps each."""
+    return {"separate": run_mobo(problem, hyper, separate=True, seed=seed),
+            "full": run_mobo(problem, hyper, separate=False, seed=seed)}

@@ -1,0 +1,43 @@
+"""The SMOKE_TEST pipeline path on the device KG (dkg_amd.bo_smoke; reference pipeline/main.py:171-216,
+bo_loop.py:48-59, 122-131, 380-450): the gp-sample problem lengthscales/0 (the committed golden
+fixture, tests/golden/make_golden.py) with the reference's fixed hyperparameters (main.py:84-88)."""
+
+import pytest
+import torch
+
+from dkg_amd.bo_smoke import GPProblem, run_smoke
+from helpers import load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HYPER = dict(length_scales=[0.2, 1.8], output_scales=[1, 50], means=[0, 0])
+
+
+def test_problem_objective_is_posterior_mean():
+    """gp_testproblem.py:76-98: objective i = posterior mean of the problem GP's output i."""
+    state, om, D, W, X, _ = load_golden("lengthscales0")
+    problem = GPProblem(state, device=DEV)
+    got = problem(X)
+    ref = torch.stack([p[0] for p in om.posterior_list(X, observation_noise=False)], dim=-1)
+    torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-9 * float(ref.abs().max()))
+
+
+def test_smoke_pipeline_runs_both_modes():
+    state, *_ = load_golden("lengthscales0")
+    problem = GPProblem(state, device=DEV)
+    res = run_smoke(problem, HYPER, seed=0)
+    sep, full = res["separate"], res["full"]
+    for h in (sep, full):
+        assert len(h["x"]) == 2
+        assert all(0.0 <= v <= 1.0 for x in h["x"] for v in x)
+        assert all(a == a for a in h["acq"])  # finite acquisition values
+    # decoupled: one objective per step, appended to that objective's data only (costs [1, 10])
+    assert all(i in (0, 1) for i in sep["obj_index"])
+    assert sum(sep["n_observations"]) == 2 * 6 + 2
+    assert all(c == (1.0 if i == 0 else 10.0) for i, c in zip(sep["obj_index"], sep["cost"]))
+    # full: every objective at every step; KG >= 0
+    assert full["n_observations"] == [8, 8]
+    assert all(a >= 0.0 for a in full["acq"])
+    # deterministic under the seed
+    again = run_smoke(GPProblem(state, device=DEV), HYPER, seed=0)
+    assert again["full"]["x"] == full["x"] and again["separate"]["x"] == sep["x"]
