@@ -971,6 +971,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   // candidate's q_i and J_i rows, gv / gm / per-wave gradient scratch, x_b.
   const int d = P->d;
   const int NP = P->max_np;
+  const int NPS = stage_len(NP);  // GRAD: LDS row stride of the candidate's q_i / J_i rows
   const double* disc = GRAD ? P->disc : nullptr;
   // test hook (DKG_PLAN_FORCE_WALK): every pair takes the list-overflow path
   const bool force_walk = __builtin_amdgcn_readfirstlane(P->debug_env) & 1;
@@ -982,8 +983,8 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     double* gb = sbuf + (size_t)SW * 2 * LC;
     sidx = reinterpret_cast<int*>(gb);
     qrow = gb + (SW * ENV_CAP + 1) / 2;
-    jrow = qrow + (size_t)M * NP;
-    sgv = jrow + (size_t)M * d * NP;                // [M][16]  d v_i / dx
+    jrow = qrow + (size_t)M * NPS;                   // rows of stride NPS: whole DMA pieces
+    sgv = jrow + (size_t)M * d * NPS;               // [M][16]  d v_i / dx
     sgm = sgv + M * DKG_MAX_DIM;                     // [M][16]  d mu_i / dx
     sgw = sgm + M * DKG_MAX_DIM;                     // [SW][64] per wave: gacc | ga0 | gvv | gtot
     sx = sgw + SW * 64;                              // [16]     x_b
@@ -1016,6 +1017,20 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       if (full || i == target) dma_to_lds(cv_src[i], lcv + (size_t)i * SLp, N, wave, SW, lane);
     }
   }
+  if constexpr (GRAD) {
+    // the candidate's q_i and J_i rows (row-major in the workspace) by LDS-DMA with the line data, so
+    // they cost no extra memory round trip; entries npi .. NP-1 are zeroed after the wait
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i < m) {
+        const int npi = pad16(P->o[i].n);
+        const size_t mat = (size_t)P->bpad * npi;
+        dma_to_lds(P->qxrm[i] + (size_t)b * npi, qrow + (size_t)i * NPS, npi, wave, SW, lane);
+        for (int dd = 0; dd < d; ++dd)
+          dma_to_lds(P->jq[i] + dd * mat + (size_t)b * npi, jrow + ((size_t)i * d + dd) * NPS, npi, wave, SW, lane);
+      }
+    }
+  }
   for (int e = threadIdx.x; e < S * m; e += blockDim.x) lw[e] = wsrc[e];
   if (threadIdx.x < m) {
 #pragma unroll
@@ -1023,19 +1038,6 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
   if constexpr (GRAD) {
     // the candidate's q_i and J_i rows (fragment-packed in the workspace)
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      if (i < m) {
-        const int npi = pad16(P->o[i].n);
-        const size_t mat = (size_t)P->bpad * npi;
-        const double* qx = P->qxrm[i] + (size_t)b * npi;
-        const double* jq = P->jq[i] + (size_t)b * npi;
-        for (int c = threadIdx.x; c < NP; c += blockDim.x) {
-          qrow[(size_t)i * NP + c] = (c < npi) ? qx[c] : 0.0;
-          for (int dd = 0; dd < d; ++dd) jrow[((size_t)i * d + dd) * NP + c] = (c < npi) ? jq[dd * mat + c] : 0.0;
-        }
-      }
-    }
     if (threadIdx.x < m * d) {
       const int i = threadIdx.x / d, dd = threadIdx.x % d;
       sgm[i * DKG_MAX_DIM + dd] = P->gmu[i][(size_t)dd * P->bpad + b];
@@ -1075,6 +1077,24 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       __syncthreads();
     }
   }
+  if constexpr (GRAD) {
+    // rows of outputs with fewer (padded) training points than the widest: zero the tail the DMA filled
+    bool tail = false;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i < m) {
+        const int npi = pad16(P->o[i].n);
+        if (npi < NP) {
+          tail = true;
+          for (int c = npi + (int)threadIdx.x; c < NP; c += blockDim.x) {
+            qrow[(size_t)i * NPS + c] = 0.0;
+            for (int dd = 0; dd < d; ++dd) jrow[((size_t)i * d + dd) * NPS + c] = 0.0;
+          }
+        }
+      }
+    }
+    if (tail) __syncthreads();  // uniform
+  }
   if (!GRAD) KST(st, 3);
 
   double* sb = sbuf + (size_t)wave * 2 * LC;
@@ -1091,7 +1111,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     for (int pidx = wave; pidx < m * d; pidx += SW) {
       const int i = pidx / d, dd = pidx % d;
       double acc = 0.0;
-      for (int c = lane; c < NP; c += 64) acc = fma(jrow[((size_t)i * d + dd) * NP + c], qrow[(size_t)i * NP + c], acc);
+      for (int c = lane; c < NP; c += 64) acc = fma(jrow[((size_t)i * d + dd) * NPS + c], qrow[(size_t)i * NPS + c], acc);
       acc = wave_sum(acc);
       if (lane == 0) sgv[i * DKG_MAX_DIM + dd] = -2.0 * acc;
     }
@@ -1333,7 +1353,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
           for (int i = 0; i < M; ++i) {
             if (i < m && wb[i] != 0.0) {
               for (int dd = 0; dd < d; ++dd) {
-                const double* jr = jrow + ((size_t)i * d + dd) * NP;
+                const double* jr = jrow + ((size_t)i * d + dd) * NPS;
                 double acc = 0.0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -1364,7 +1384,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
                 if (c + 64 * q < npi) uw[c + 64 * q] = u[q] * wb[i];
             }
             for (int dd = 0; dd < d; ++dd) {
-              const double* jr = jrow + ((size_t)i * d + dd) * NP;
+              const double* jr = jrow + ((size_t)i * d + dd) * NPS;
               double acc = 0.0;
               for (int c = lane; c < npi; c += 64) acc = fma(jr[c], uw[c], acc);
               acc = wave_sum(acc);

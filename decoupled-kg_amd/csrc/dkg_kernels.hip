@@ -483,7 +483,8 @@ size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad
 
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream) {
   const int M = outputs_bucket(m);
-  const size_t extra = (size_t)(waves * ENV_CAP + 1) / 2 + (size_t)M * max_np + (size_t)M * d * max_np +
+  const size_t extra = (size_t)(waves * ENV_CAP + 1) / 2 + (size_t)M * stage_len(max_np) +
+                       (size_t)M * d * stage_len(max_np) +
                        2 * (size_t)M * DKG_MAX_DIM + (size_t)waves * 64 + DKG_MAX_DIM +
                        (size_t)M * DKG_MAX_DIM + (size_t)waves * (HCAP + max_np + ENV_CAP) +
                        (size_t)(waves * HCAP + 1) / 2;
