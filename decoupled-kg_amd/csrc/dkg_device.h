@@ -999,6 +999,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   // per-output scalars and the candidate's own posterior (variance from the
   // covariance stage, mean from the cross stage): lane i of wave 0 loads output i
   double pp[6] = {1.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double g_gm[M], g_il[M], g_x = 0.0;  // GRAD: staged to LDS after the wait
   if (threadIdx.x < m) {
     const dkg_output* o = &P->o[threadIdx.x];
     pp[0] = o->y_std;
@@ -1037,16 +1038,18 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     for (int q = 0; q < 6; ++q) s_pp[threadIdx.x * 6 + q] = pp[q];
   }
   if constexpr (GRAD) {
-    // the candidate's q_i and J_i rows (fragment-packed in the workspace)
-    if (threadIdx.x < m * d) {
-      const int i = threadIdx.x / d, dd = threadIdx.x % d;
-      sgm[i * DKG_MAX_DIM + dd] = P->gmu[i][(size_t)dd * P->bpad + b];
+    // d mu_i/dx, 1/lengthscale and x_b into registers: per-output pointers by scalar loads (lgkmcnt,
+    // not queued behind the DMAs on vmcnt), the values stored to LDS after the staging wait
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      g_gm[i] = 0.0;
+      g_il[i] = 0.0;
+      if (i < m && threadIdx.x < d) {
+        g_gm[i] = P->gmu[i][(size_t)threadIdx.x * P->bpad + b];
+        g_il[i] = P->o[i].inv_lengthscale[threadIdx.x];
+      }
     }
-    if (threadIdx.x < d) sx[threadIdx.x] = xnew[(size_t)b * d + threadIdx.x];
-    if (threadIdx.x < m * d) {
-      const int i = threadIdx.x / d, dd = threadIdx.x % d;
-      sil[i * DKG_MAX_DIM + dd] = P->o[i].inv_lengthscale[dd];
-    }
+    if (threadIdx.x < d) g_x = xnew[(size_t)b * d + threadIdx.x];
   }
   // Padding lines k = N+1 .. 64*MAXL-1 (read at indices N .. 64*MAXL-2) come
   // out of the branch-free line build as (a = NaN, b = b_0): mu = NaN makes
@@ -1078,6 +1081,16 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     }
   }
   if constexpr (GRAD) {
+    if (threadIdx.x < d) {
+      sx[threadIdx.x] = g_x;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (i < m) {
+          sgm[i * DKG_MAX_DIM + threadIdx.x] = g_gm[i];
+          sil[i * DKG_MAX_DIM + threadIdx.x] = g_il[i];
+        }
+      }
+    }
     // rows of outputs with fewer (padded) training points than the widest: zero the tail the DMA filled
     bool tail = false;
 #pragma unroll
