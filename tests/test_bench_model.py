@@ -1,0 +1,43 @@
+"""bench.py's algorithmic cost models against the figures SURVEY.md §8(d) / BASELINE.md state for them
+(CPU only: the models are arithmetic)."""
+
+import importlib.util
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(HERE), "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_survey_model_matches_survey_figures():
+    b = _bench()
+    # headline: m=2, n=256, N=1024, S=16, B=128, d=2 -> 1.53 MFLOP per KG-eval, 5.29 MB per batch
+    f, by = b.survey_model(2, [256, 256], 1024, 16, 128, 2)
+    assert abs(f / 128 - 1.527e6) / 1.527e6 < 1e-3
+    assert abs(by - 5.287e6) / 5.287e6 < 1e-3
+    # small: 0.11 MFLOP per eval; stress: 33.8 MFLOP per eval
+    f_small, _ = b.survey_model(2, [64, 64], 256, 8, 32, 2)
+    assert abs(f_small / 32 - 0.11e6) / 0.11e6 < 0.05
+    f_stress, _ = b.survey_model(3, [1024] * 3, 4096, 32, 256, 2)
+    assert abs(f_stress / 256 - 33.8e6) / 33.8e6 < 0.01
+    # the headline forward's fp64 floor: max(F/78.6 TF, bytes/8 TB/s) ~ 2.49 us
+    t_min = max(f / 78.6e12, by / 8e12)
+    assert 2.4e-6 < t_min < 2.6e-6
+
+
+def test_stage_model_matches_design_table():
+    """DESIGN.md §4's per-launch table: 17.9 / 137.9 / 21.0 MFLOP at the headline."""
+    b = _bench()
+
+    class W:
+        m, S, d = 2, 16, 2
+
+    st = b.stage_model(W, 2, [256, 256], 1024, 128, 16, 2)
+    assert abs(st["cross_root_kernel"][0] / 1e6 - 17.9) < 0.1
+    assert abs(st["posterior_cov_kernel"][0] / 1e6 - 137.9) < 0.1
+    assert abs(st["envelope_kernel"][0] / 1e6 - 21.0) < 0.1
