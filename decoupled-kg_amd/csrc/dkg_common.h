@@ -184,6 +184,16 @@ __device__ __forceinline__ double partner_f64(double v) {
     { constexpr int S_ = 5; __VA_ARGS__ }          \
   }
 
+// The four in-row steps only: afterwards every lane of a 16-lane row holds its
+// row's combine.
+#define DKG_BUTTERFLY_ROW(...)                     \
+  {                                                \
+    { constexpr int S_ = 0; __VA_ARGS__ }          \
+    { constexpr int S_ = 1; __VA_ARGS__ }          \
+    { constexpr int S_ = 2; __VA_ARGS__ }          \
+    { constexpr int S_ = 3; __VA_ARGS__ }          \
+  }
+
 // v_min_f64 / v_max_f64 without the operand canonicalisation LLVM puts in
 // front of fmin/fmax (one extra VALU op per operand).  The kernels run in IEEE
 // mode, where a quiet-NaN operand yields the other operand: exactly fmin/fmax
@@ -205,9 +215,22 @@ __device__ __forceinline__ double keep_or_qnan(bool c, double v) {
   return __hiloint2double(c ? __double2hiint(v) : 0x7FF80000, __double2loint(v));
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int l);
+
+// Cross-row combine after DKG_BUTTERFLY_ROW: the four row values by v_readlane
+// (scalar registers, no LDS round trip as the ds_bpermute steps 16/32 take),
+// combined in a fixed order, (r0 op r1) op (r2 op r3): wave-uniform and
+// deterministic.
+template <class Op>
+__device__ __forceinline__ double combine_rows(double v, Op op) {
+  const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
+  const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+  return op(op(r0, r1), op(r2, r3));
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-  DKG_BUTTERFLY({ v = v + partner_f64<S_>(v); })
-  return v;
+  DKG_BUTTERFLY_ROW({ v = v + partner_f64<S_>(v); })
+  return combine_rows(v, [](double a, double b) { return a + b; });
 }
 
 __device__ __forceinline__ double wave_max(double v) {

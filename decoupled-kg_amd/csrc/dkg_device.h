@@ -157,11 +157,14 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
     bmax = fmax_raw(bmax, lb[t]);
     amax = fmax_raw(amax, la[t]);
   }
-  DKG_BUTTERFLY({
+  DKG_BUTTERFLY_ROW({
     bmin = fmin_raw(bmin, partner_f64<S_>(bmin));
     bmax = fmax_raw(bmax, partner_f64<S_>(bmax));
     amax = fmax_raw(amax, partner_f64<S_>(amax));
   })
+  bmin = combine_rows(bmin, [](double a, double b) { return fmin(a, b); });
+  bmax = combine_rows(bmax, [](double a, double b) { return fmax(a, b); });
+  amax = combine_rows(amax, [](double a, double b) { return fmax(a, b); });
   // short-circuit of discretekg.py:363-367 (all |b| < 1e-9), and the
   // single-slope case (one hull vertex, E = max a): KG = 0.
   if (!uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax)) {
@@ -175,11 +178,14 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
     aR = fmax_raw(aR, keep_or_qnan(lb[t] == bmax, la[t]));
     bT = fmin_raw(bT, keep_or_qnan(la[t] == amax, lb[t]));
   }
-  DKG_BUTTERFLY({
+  DKG_BUTTERFLY_ROW({
     aL = fmax_raw(aL, partner_f64<S_>(aL));
     aR = fmax_raw(aR, partner_f64<S_>(aR));
     bT = fmin_raw(bT, partner_f64<S_>(bT));
   })
+  aL = combine_rows(aL, [](double a, double b) { return fmax(a, b); });
+  aR = combine_rows(aR, [](double a, double b) { return fmax(a, b); });
+  bT = combine_rows(bT, [](double a, double b) { return fmin(a, b); });
   const double bL = bmin, bR = bmax, aT = amax;
   f.bL = bL; f.aL = aL; f.bR = bR; f.aR = aR; f.bT = bT; f.aT = aT;
 
