@@ -228,14 +228,25 @@ __device__ __forceinline__ double combine_rows(double v, Op op) {
   return op(op(r0, r1), op(r2, r3));
 }
 
+// Wave minimum of an int: the four in-row DPP steps, then the four row values by v_readlane.
+__device__ __forceinline__ int wave_min_i32(int v) {
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));
+  const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+  const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+  return min(min(r0, r1), min(r2, r3));
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
   DKG_BUTTERFLY_ROW({ v = v + partner_f64<S_>(v); })
   return combine_rows(v, [](double a, double b) { return a + b; });
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-  DKG_BUTTERFLY({ v = fmax(v, partner_f64<S_>(v)); })
-  return v;
+  DKG_BUTTERFLY_ROW({ v = fmax(v, partner_f64<S_>(v)); })
+  return combine_rows(v, [](double a, double b) { return fmax(a, b); });
 }
 
 // A condition every lane agrees on, made visibly wave-uniform (scalar branch,

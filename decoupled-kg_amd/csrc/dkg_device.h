@@ -354,10 +354,7 @@ __device__ __forceinline__ HullGrad envelope_hull_grad(const EnvFilter& f, int l
     if (ok[c] && lb_[c] == f.bL && la_[c] == f.aL) kst = min(kst, li_[c]);
     cntT += __popcll(__ballot(ok[c] && la_[c] == f.aT));
   }
-  DKG_BUTTERFLY({
-    const int o = __shfl_xor(kst, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
-    kst = min(kst, o);
-  })
+  kst = wave_min_i32(kst);
   int start;
   {
     const uint64_t m0 = __ballot(ok[0] && li_[0] == kst), m1 = __ballot(ok[1] && li_[1] == kst);
