@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-reps", type=int, default=50)
+    ap.add_argument("--streams", type=int, default=4,
+                    help="forward batches in flight: step k runs on stream k %% streams with its own plan workspace")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_headline.json"),
                     help="per-kernel HBM traffic from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
@@ -149,35 +151,65 @@ def main():
     from dkg_amd.dist import BatchExchange
     xchg = BatchExchange(w.B, E, "gather" if args.shard == "candidates" else "reduce", S_local=w.S, device=dev)
 
-    def step(k):
-        kg = xchg.row(k)
-        plan.forward_into(Xd, kg)
-        xchg.done(k)
-        return kg
+    main_s = torch.cuda.current_stream(dev)
 
-    for k in range(args.warmup):
-        step(k)
-    xchg.flush(args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for k in range(args.steps):
-        step(k)
-    xchg.flush(args.steps)
-    ev1.record()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    gpu_s = ev0.elapsed_time(ev1) / 1e3
-    t = torch.tensor([max(wall, gpu_s)], dtype=torch.double, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t)
+    def timed(ns, steps, warmup):
+        """Warmup + `steps` timed forwards with `ns` forward batches in flight.  Stream i (i = k % ns)
+        runs step k through its own plan (own Q_X / cov workspace); a stream waits on the main stream
+        whenever a new exchange buffer starts, and the main stream waits on every stream before an
+        exchange, so each collective sees completed rows and a row is never rewritten under one."""
+        streams = [main_s] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+        plans = [plan] + [acq._state.plan(acq._W, acq.target_output_ix, plan.max_B, f32=args.precision == "fp32")
+                          for _ in range(ns - 1)]
+
+        def join():
+            for s in streams[1:]:
+                main_s.wait_stream(s)
+
+        def step(k):
+            kg = xchg.row(k)
+            if ns > 1 and k % E == 0:
+                for s in streams[1:]:
+                    s.wait_stream(main_s)
+            with torch.cuda.stream(streams[k % ns]):
+                plans[k % ns].forward_into(Xd, kg)
+            if k % E == E - 1:
+                join()
+            xchg.done(k)
+
+        for k in range(warmup):
+            step(k)
+        join()
+        xchg.flush(warmup)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for s in streams[1:]:
+            s.wait_stream(main_s)
+        for k in range(steps):
+            step(k)
+        join()
+        xchg.flush(steps)
+        ev1.record()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        gpu_s = ev0.elapsed_time(ev1) / 1e3
+        t = torch.tensor([max(wall, gpu_s)], dtype=torch.double, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t)
+
+    single = None
+    if args.streams > 1:
+        e1 = timed(1, args.steps, args.warmup)
+        single = {"value": world * w.B * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
+    elapsed = timed(max(1, args.streams), args.steps, args.warmup)
     value = world * w.B * args.steps / elapsed
 
     # ---- per-kernel durations (HIP events on the launch stream), roofline of the dominant kernel
@@ -259,7 +291,8 @@ def main():
                        "parallelism": f"{args.shard} sharded over {world} GPU(s); one async RCCL "
                                       f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'} "
                                       f"per {E} forward batches",
-                       "exchange_every": E},
+                       "exchange_every": E, "streams": max(1, args.streams)},
+            "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
             "roofline": roof,

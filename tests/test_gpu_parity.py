@@ -432,3 +432,38 @@ def test_envelope_sizes_match_reference_walk(workload, nX):
     # near-collinear vertices may be classified differently under the two roundings of the lines
     assert agree >= 0.95 and int((got - ref).abs().max()) <= 2, f"agree {agree:.3f}, ref {ref.tolist()}, got {got.tolist()}"
     torch.testing.assert_close(pairs.mean(-1), kg, rtol=1e-12, atol=1e-300)
+
+
+def test_concurrent_plans_on_streams_match_single_stream():
+    """bench.py's --streams path: four plans (own Q_X / cov workspace each) run interleaved batches on
+    four HIP streams; every batch's KG is bit-identical to the same batch run alone on one stream."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    w = WORKLOADS["headline"]
+    model, D, X, W = make_problem(w)
+    dev = torch.device("cuda", 0)
+    acq = DiscreteKnowledgeGradient(model, D, W, device=dev)
+    base = acq._plan_for(w.B)
+    batches = [torch.quasirandom.SobolEngine(w.d, scramble=True, seed=11 + k).draw(w.B, dtype=torch.double)
+               .to(dev).contiguous() for k in range(12)]
+    want = []
+    for Xb in batches:
+        kg = torch.empty(w.B, dtype=torch.double, device=dev)
+        base.forward_into(Xb, kg)
+        want.append(kg)
+    torch.cuda.synchronize()
+    main = torch.cuda.current_stream(dev)
+    streams = [main] + [torch.cuda.Stream(dev) for _ in range(3)]
+    plans = [base] + [acq._state.plan(acq._W, acq.target_output_ix, base.max_B) for _ in range(3)]
+    got = torch.full((len(batches), w.B), float("nan"), dtype=torch.double, device=dev)
+    for s in streams[1:]:
+        s.wait_stream(main)
+    for k, Xb in enumerate(batches):
+        with torch.cuda.stream(streams[k % 4]):
+            plans[k % 4].forward_into(Xb, got[k])
+    for s in streams[1:]:
+        main.wait_stream(s)
+    torch.cuda.synchronize()
+    for k in range(len(batches)):
+        assert torch.equal(got[k], want[k]), k
