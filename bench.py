@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--profile-reps", type=int, default=50)
     ap.add_argument("--streams", type=int, default=4,
                     help="forward batches in flight: step k runs on stream k %% streams with its own plan workspace")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1 = replay each full exchange period (E forwards over the streams) as one captured HIP graph")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_headline.json"),
                     help="per-kernel HBM traffic from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
@@ -153,7 +155,7 @@ def main():
 
     main_s = torch.cuda.current_stream(dev)
 
-    def timed(ns, steps, warmup):
+    def timed(ns, steps, warmup, graph=False):
         """Warmup + `steps` timed forwards with `ns` forward batches in flight.  Stream i (i = k % ns)
         runs step k through its own plan (own Q_X / cov workspace); a stream waits on the main stream
         whenever a new exchange buffer starts, and the main stream waits on every stream before an
@@ -182,6 +184,25 @@ def main():
         join()
         xchg.flush(warmup)
         torch.cuda.synchronize()
+
+        graphs = []
+        if graph and steps >= E:
+            # one graph per exchange buffer: the E forwards of a period, forked over the streams exactly
+            # as the eager path does; replayed on the main stream, so the collective after it orders as before
+            for slot in range(2):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    cs = torch.cuda.current_stream(dev)
+                    lanes = [cs] + streams[1:]
+                    for s in lanes[1:]:
+                        s.wait_stream(cs)
+                    for r in range(E):
+                        with torch.cuda.stream(lanes[r % ns]):
+                            plans[r % ns].forward_into(Xd, xchg.bufs[slot][r])
+                    for s in lanes[1:]:
+                        cs.wait_stream(s)
+                graphs.append(g)
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -190,7 +211,14 @@ def main():
         ev0.record()
         for s in streams[1:]:
             s.wait_stream(main_s)
-        for k in range(steps):
+        k0 = 0
+        if graphs:
+            while k0 + E <= steps:
+                xchg.row(k0)
+                graphs[(k0 // E) % 2].replay()
+                xchg.done(k0 + E - 1)
+                k0 += E
+        for k in range(k0, steps):
             step(k)
         join()
         xchg.flush(steps)
@@ -206,10 +234,10 @@ def main():
         return float(t)
 
     single = None
-    if args.streams > 1:
+    if args.streams > 1 or args.graph:
         e1 = timed(1, args.steps, args.warmup)
         single = {"value": world * w.B * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
-    elapsed = timed(max(1, args.streams), args.steps, args.warmup)
+    elapsed = timed(max(1, args.streams), args.steps, args.warmup, graph=bool(args.graph))
     value = world * w.B * args.steps / elapsed
 
     # ---- per-kernel durations (HIP events on the launch stream), roofline of the dominant kernel
@@ -291,7 +319,8 @@ def main():
                        "parallelism": f"{args.shard} sharded over {world} GPU(s); one async RCCL "
                                       f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'} "
                                       f"per {E} forward batches",
-                       "exchange_every": E, "streams": max(1, args.streams)},
+                       "exchange_every": E, "streams": max(1, args.streams),
+                       "hip_graph": bool(args.graph)},
             "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,

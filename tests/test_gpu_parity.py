@@ -435,7 +435,7 @@ def test_envelope_sizes_match_reference_walk(workload, nX):
 
 
 def test_concurrent_plans_on_streams_match_single_stream():
-    """bench.py's --streams path: four plans (own Q_X / cov workspace each) run interleaved batches on
+    """bench.py's --streams / --graph path: four plans (own Q_X / cov workspace each) run interleaved batches on
     four HIP streams; every batch's KG is bit-identical to the same batch run alone on one stream."""
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
@@ -467,3 +467,23 @@ def test_concurrent_plans_on_streams_match_single_stream():
     torch.cuda.synchronize()
     for k in range(len(batches)):
         assert torch.equal(got[k], want[k]), k
+
+    # bench.py --graph: the same interleaving captured once as a HIP graph, replayed twice
+    got.fill_(float("nan"))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cs = torch.cuda.current_stream(dev)
+        lanes = [cs] + streams[1:]
+        for s in lanes[1:]:
+            s.wait_stream(cs)
+        for k, Xb in enumerate(batches):
+            with torch.cuda.stream(lanes[k % 4]):
+                plans[k % 4].forward_into(Xb, got[k])
+        for s in lanes[1:]:
+            cs.wait_stream(s)
+    for _ in range(2):
+        got.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        for k in range(len(batches)):
+            assert torch.equal(got[k], want[k]), k
