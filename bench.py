@@ -44,7 +44,7 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=1024)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", default="headline")
     ap.add_argument("--shard", choices=["candidates", "scalarisations"], default="candidates",
