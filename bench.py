@@ -191,7 +191,8 @@ def main():
             # as the eager path does; replayed on the main stream, so the collective after it orders as before
             for slot in range(2):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                # thread_local: the RCCL watchdog thread may query events while this thread captures
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     cs = torch.cuda.current_stream(dev)
                     lanes = [cs] + streams[1:]
                     for s in lanes[1:]:
