@@ -41,3 +41,13 @@ def test_stage_model_matches_design_table():
     assert abs(st["cross_root_kernel"][0] / 1e6 - 17.9) < 0.1
     assert abs(st["posterior_cov_kernel"][0] / 1e6 - 137.9) < 0.1
     assert abs(st["envelope_kernel"][0] / 1e6 - 21.0) < 0.1
+
+
+def test_default_run_is_whole_graph_periods(monkeypatch):
+    """The default bench line: four forward batches in flight, graph replay on, and a step count that is
+    a whole number of exchange periods, so no timed step falls back to eager launches."""
+    b = _bench()
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    a = b.parse()
+    assert a.gpus == 1 and a.streams == 4 and a.graph == 1
+    assert a.steps % a.exchange_every == 0
