@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--workload", default="headline")
     ap.add_argument("--shard", choices=["candidates", "scalarisations"], default="candidates",
                     help="axis of the (candidate x scalarisation) space split over ranks (weak scaling)")
-    ap.add_argument("--exchange-every", type=int, default=64,
+    ap.add_argument("--exchange-every", type=int, default=256,
                     help="forward batches per RCCL exchange (count = K*B fp64 values)")
     ap.add_argument("--target", type=int, default=None, help="target_output_ix (decoupled path); default full")
     ap.add_argument("--precision", choices=["fp64", "fp32"], default="fp64",
