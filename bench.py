@@ -124,10 +124,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # DKG_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with several ranks on one GPU (not a bench line)
+    backend = os.environ.get("DKG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
