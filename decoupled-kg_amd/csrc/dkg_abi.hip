@@ -472,9 +472,48 @@ int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, d
   if (P == 0) return DKG_OK;
   if (L == 0)
     return fail(DKG_ERR_NO_LINES, "Expected inputs to specify at least one line. Got intercepts.shape[-1]=0.");
-  if (L > 64 * 33) return fail(DKG_ERR_UNSUPPORTED, "L=%d lines per set (supported <= %d)", L, 64 * 33);
   if (!intercepts || !slopes || !kg) return fail(DKG_ERR_ARG, "NULL pointer");
-  return hip_check(launch_lines_kg(intercepts, slopes, P, L, kg, n_hull, (hipStream_t)stream), "lines_kg_kernel");
+  return hip_check(launch_lines_kg(intercepts, slopes, P, L, kg, n_hull, nullptr, nullptr, 0, (hipStream_t)stream),
+                   "lines_kg_kernel");
+}
+
+int dkg_epigraph(const double* intercepts, const double* slopes, int P, int L, int cap, long long* indices,
+                 double* intersections, int* count, void* stream) {
+  if (P < 0 || L < 0 || cap < 1) return fail(DKG_ERR_ARG, "bad size P=%d L=%d cap=%d", P, L, cap);
+  if (P == 0) return DKG_OK;
+  if (L == 0)
+    return fail(DKG_ERR_NO_LINES, "Expected inputs to specify at least one line. Got intercepts.shape[-1]=0.");
+  if (!intercepts || !slopes || !indices || !count || (cap > 1 && !intersections))
+    return fail(DKG_ERR_ARG, "NULL pointer");
+  return hip_check(launch_lines_kg(intercepts, slopes, P, L, nullptr, count, indices, intersections, cap,
+                                   (hipStream_t)stream), "lines_kg_kernel(epigraph)");
+}
+
+int dkg_pwl_expectation(const double* intercepts, const double* slopes, const double* boundaries, int P, int m,
+                        double* out, void* stream) {
+  if (P < 0 || m < 0) return fail(DKG_ERR_ARG, "negative size P=%d m=%d", P, m);
+  if (P == 0) return DKG_OK;
+  if (m == 0)
+    return fail(DKG_ERR_NO_LINES, "Expected inputs to specify at least one line. Got intercepts.shape[-1]=0.");
+  if (!intercepts || !slopes || !out || (m > 1 && !boundaries)) return fail(DKG_ERR_ARG, "NULL pointer");
+  return hip_check(launch_pwl_expectation(intercepts, slopes, boundaries, P, m, out, (hipStream_t)stream),
+                   "pwl_expectation_kernel");
+}
+
+int dkg_plan_lines(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* intercepts,
+                   double* slopes, void* stream) {
+  if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  if (B < 0 || B > h.max_B) return fail(DKG_ERR_ARG, "B=%d outside [0, %d]", B, h.max_B);
+  if (B == 0) return DKG_OK;
+  if (!xnew || !intercepts || !slopes) return fail(DKG_ERR_ARG, "NULL data pointer");
+  if (h.f32) return fail(DKG_ERR_UNSUPPORTED, "dkg_plan_lines needs an fp64 plan");
+  const Plan* dev = static_cast<const Plan*>(dev_plan);
+  hipStream_t s = (hipStream_t)stream;
+  int st;
+  for (int stage = 0; stage < 2; ++stage)  // K(x, X) R, means; covariance rows, variances (kg is only zeroed)
+    if ((st = hip_check(launch_stage(h, dev, xnew, B, intercepts, nullptr, s, stage), "stage"))) return st;
+  return hip_check(launch_lines_export(h, dev, B, intercepts, slopes, s), "lines_export_kernel");
 }
 
 int dkg_debug_read_kstamps(unsigned long long* host, int n) {

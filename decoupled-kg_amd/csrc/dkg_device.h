@@ -8,6 +8,7 @@
 
 #include "dkg_common.h"
 #include "dkg_kernels.h"
+#include "dkg_walk.h"
 
 namespace dkg {
 
@@ -73,48 +74,6 @@ constexpr int VCAP = 64;
 __host__ __device__ constexpr int list_cap(bool refine) { return refine ? LIST_CAP_STREAM : ENV_CAP; }
 // LDS doubles per wave for the refinement's vertex arrays (vb, va, vn)
 constexpr int VREG = 3 * VCAP;
-
-// Gift wrap over all register lines (fallback when the survivor list
-// overflows ENV_CAP): next vertex = argmin of the next intersection, found by
-// a wave butterfly per hull step.
-template <int MAXL>
-__device__ __forceinline__ double envelope_walk(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
-                                             double bL, double aL, double bR, double bT, int* nhull) {
-  double bc = bL, ac = aL, kg = 0.0;
-  int h = 1;
-  for (int guard = 0; guard <= nl && uniform(bc < bR); ++guard) {
-    double bn = INFINITY, bd = 1.0, bbest = -INFINITY, abest = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      const double bb = lb[t], a = la[t];
-      if (lane + 64 * t < nl && bb > bc) {
-        const double num = ac - a, den = bb - bc;
-        const double lhs = num * bd, rhs = bn * den;
-        if (bbest == -INFINITY || lhs < rhs || (lhs == rhs && bb > bbest)) { bn = num; bd = den; bbest = bb; abest = a; }
-      }
-    }
-    DKG_BUTTERFLY({
-      const double on = partner_f64<S_>(bn), od = partner_f64<S_>(bd);
-      const double ob = partner_f64<S_>(bbest), oa = partner_f64<S_>(abest);
-      bool take;
-      if (ob == -INFINITY) take = false;
-      else if (bbest == -INFINITY) take = true;
-      else {
-        const double lhs = on * bd, rhs = bn * od;
-        take = lhs < rhs || (lhs == rhs && (ob > bbest || (ob == bbest && oa > abest)));
-      }
-      if (take) { bn = on; bd = od; bbest = ob; abest = oa; }
-    })
-    if (!uniform(bbest > bc)) break;
-    const double c = bn / bd;
-    kg += (bbest - bc) * psi((bbest <= bT) ? -c : c);
-    bc = bbest;
-    ac = abest;
-    ++h;
-  }
-  if (nhull) *nhull = h;
-  return kg;
-}
 
 // Result of the register passes over one set of lines.
 struct EnvFilter {
@@ -229,85 +188,142 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
   return f;
 }
 
-// Exact upper envelope of the candidate list (survivors + L, T, R) and the
-// cancellation-free expectation; needs no register lines.
-__device__ __forceinline__ double envelope_hull(const EnvFilter& f, int lane, double* sb, double* sa, int* nhull,
-                                                int /*unused*/ = 0) {
-  const int cnt = f.cnt;
-  const double bT = f.bT;
-  if (lane == 0) {
-    sb[cnt] = f.bL; sa[cnt] = f.aL;
-    sb[cnt + 1] = f.bT; sa[cnt + 1] = f.aT;
-    sb[cnt + 2] = f.bR; sa[cnt + 2] = f.aR;
-  }
-  const int nc = cnt + 3;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // ---- right neighbour of every candidate P (one per lane, two chunks of 64
-  // at most): the line that takes over from P as z grows, i.e. the reference
-  // walk's step (discretekg.py:382-401): argmin over b_Q > b_P of the
-  // intersection (a_P - a_Q)/(b_Q - b_P), ties -> larger slope.  Compared by
-  // cross multiplication (both denominators > 0).  The list is read from LDS
-  // once; candidate Q = j is broadcast from lane j's register (v_readlane),
-  // and the selection is branch-free.
-  double lb_[2], la_[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int e = min(c * 64 + lane, nc - 1);
-    lb_[c] = sb[e];
-    la_[c] = sa[e];
-  }
-  int nxt[2] = {-1, -1};
-  double cn[2] = {0.0, 0.0}, cd[2] = {1.0, 1.0}, cb[2] = {0.0, 0.0}, pb[2] = {0.0, 0.0};
-  const int nc0 = min(nc, 64);
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    if (c * 64 >= nc) break;
-    const double bP = lb_[c], aP = la_[c];
-    double rn = 0.0, rd = 1.0, rb = 0.0;
-    int rj = -1;
-    auto consider = [&](double bQ, double aQ, int j) {
-      const double num = aP - aQ, den = bQ - bP;
-      const double x = num * rd, y = rn * den;
-      const bool take = (den > 0.0) & ((rj < 0) | (x < y) | ((x == y) & (bQ > rb)));
-      rn = take ? num : rn;
-      rd = take ? den : rd;
-      rb = take ? bQ : rb;
-      rj = take ? j : rj;
-    };
-#pragma unroll 4
-    for (int j = 0; j < nc0; ++j) consider(readlane_f64(lb_[0], j), readlane_f64(la_[0], j), j);
-    for (int j = 64; j < nc; ++j) consider(readlane_f64(lb_[1], j - 64), readlane_f64(la_[1], j - 64), j);
-    nxt[c] = rj; cn[c] = rn; cd[c] = rd; cb[c] = rb; pb[c] = bP;
-  }
+// ---------------------------------------------------------------------------
+// Forward envelope of one set of lines (one (candidate, scalarisation) pair,
+// or one set of dkg_lines_kg / dkg_epigraph): extremes, the margin chord
+// filter into the wave's LDS list (slope, intercept, line index), and the
+// reference's walk over that list (dkg_walk.h), redone over all lines when
+// the list overflows or a breakpoint leaves WALK_XGUARD.
 
-  // ---- follow the chain from L (index cnt): its members are the envelope
-  // lines in increasing slope, ending at R (no right neighbour).
-  uint64_t on0 = 0, on1 = 0;
-  int h = 0;
-  for (int cur = cnt, guard = 0; cur >= 0 && guard < nc; ++guard) {
-    if (cur < 64) on0 |= 1ull << cur; else on1 |= 1ull << (cur - 64);
-    ++h;
-    cur = (cur < 64) ? __builtin_amdgcn_readlane(nxt[0], cur) : __builtin_amdgcn_readlane(nxt[1], cur - 64);
-  }
-  // ---- each envelope line other than R contributes its right edge P -> Q:
-  //   (b_Q - b_P) psi(+-c), minus sign when the edge ends at or left of T.
-  double v = 0.0;
+struct FwdEnv {
+  double bL, aL, bR, aR, bT, aT;
+  int cnt;     // list entries (may exceed the capacity: overflow)
+  int status;  // 0: list ready, 1: KG = 0 (short-circuit or one slope), 2: overflow
+};
+
+// Extremes with their exact ties over register lines: L = min b (tie: max a),
+// R = max b (tie: max a), T = max a (tie: min b).  Padding slots hold lines
+// with a NaN intercept, which drop out of every raw min / max (IEEE maxNum)
+// and fail every comparison.  status 1: every |b| < 1e-9 (discretekg.py:363-367)
+// or a single slope (the walk stops at its first line): KG = 0, one line.
+template <int MAXL>
+__device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const double (&lb)[MAXL]) {
+  FwdEnv f;
+  double bmin = INFINITY, bmax = -INFINITY, amax = -INFINITY;
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    if (c * 64 >= nc) break;
-    const bool on = (((c == 0) ? on0 : on1) >> lane) & 1;
-    if (on && nxt[c] >= 0) {
-      const double cc = cn[c] / cd[c];
-      const double sc = (cb[c] <= bT) ? -cc : cc;
-      v += (cb[c] - pb[c]) * psi(sc);
-    }
+  for (int t = 0; t < MAXL; ++t) {
+    bmin = fmin_raw(bmin, lb[t]);
+    bmax = fmax_raw(bmax, lb[t]);
+    amax = fmax_raw(amax, la[t]);
   }
-  if (nhull) *nhull = h;
-  return wave_sum(v);
+  DKG_BUTTERFLY_ROW({
+    bmin = fmin_raw(bmin, partner_f64<S_>(bmin));
+    bmax = fmax_raw(bmax, partner_f64<S_>(bmax));
+    amax = fmax_raw(amax, partner_f64<S_>(amax));
+  })
+  bmin = combine_rows(bmin, [](double a, double b) { return fmin(a, b); });
+  bmax = combine_rows(bmax, [](double a, double b) { return fmax(a, b); });
+  amax = combine_rows(amax, [](double a, double b) { return fmax(a, b); });
+  f.bL = bmin; f.bR = bmax; f.aT = amax;
+  f.cnt = 0;
+  if (!uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax)) {
+    f.status = 1;
+    return f;
+  }
+  double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    aL = fmax_raw(aL, keep_or_qnan(lb[t] == bmin, la[t]));
+    aR = fmax_raw(aR, keep_or_qnan(lb[t] == bmax, la[t]));
+    bT = fmin_raw(bT, keep_or_qnan(la[t] == amax, lb[t]));
+  }
+  DKG_BUTTERFLY_ROW({
+    aL = fmax_raw(aL, partner_f64<S_>(aL));
+    aR = fmax_raw(aR, partner_f64<S_>(aR));
+    bT = fmin_raw(bT, partner_f64<S_>(bT));
+  })
+  f.aL = combine_rows(aL, [](double a, double b) { return fmax(a, b); });
+  f.aR = combine_rows(aR, [](double a, double b) { return fmax(a, b); });
+  f.bT = combine_rows(bT, [](double a, double b) { return fmin(a, b); });
+  f.status = 0;
+  return f;
 }
 
+// The margin chord filter (EnvChords) over register lines into the list
+// (capacity CAP entries; the count goes on past it).
+template <int MAXL, int CAP>
+__device__ __forceinline__ int env_compact(const double (&la)[MAXL], const double (&lb)[MAXL], const EnvChords& ch,
+                                           int lane, double* sb, double* sa, int* si) {
+  int cnt = 0;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    const double a = la[t], bb = lb[t];
+    const bool s = env_keep(ch, a, bb);
+    const uint64_t mk = __ballot(s);
+    if (mk != 0) {  // wave-uniform, rarely taken
+      if (s) {
+        const int pos = cnt + lanes_below(mk);
+        if (pos < CAP) {
+          sb[pos] = bb;
+          sa[pos] = a;
+          si[pos] = lane + 64 * t;
+        }
+      }
+      cnt += __popcll(mk);
+    }
+  }
+  return cnt;
+}
+
+// Short-circuit index (dkg_epigraph): the first line attaining max a
+// (torch.max over the intercepts, discretekg.py:366).
+template <int MAXL>
+__device__ __forceinline__ int first_max_index(const double (&la)[MAXL], int nl, int lane, double amax) {
+  int k = KEY_NONE;
+#pragma unroll
+  for (int t = MAXL - 1; t >= 0; --t) k = (lane + 64 * t < nl && la[t] == amax) ? lane + 64 * t : k;
+  return wave_min_i32(k);
+}
+
+// KG_w (and the envelope size) of register-held lines: build(la, lb) fills the
+// lines (line k in lane k % 64, slot k / 64; k >= nl: NaN intercepts); it runs
+// again only for the overflow walk, so no register line is live across the
+// list walk.  force_walk: test hook (every set takes the walk over all lines).
+template <int MAXL, class Build>
+__device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
+                                                bool force_walk, int* nhull, const WalkOut* out = nullptr) {
+  FwdEnv f;
+  {
+    double la[MAXL], lb[MAXL];
+    build(la, lb);
+    f = env_extremes<MAXL>(la, lb);
+    if (f.status == 1) {
+      if (out && out->cap > 0) {
+        const int k = first_max_index<MAXL>(la, nl, lane, f.aT);
+        if (lane == 0) out->idx[0] = k;
+      }
+      *nhull = 1;
+      return 0.0;
+    }
+    f.cnt = env_compact<MAXL, ENV_CAP>(la, lb, env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR), lane, sb, sa, si);
+  }
+  if (f.cnt <= ENV_CAP && !force_walk) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double cmax;
+    int h;
+    const double kg = (f.cnt <= 64) ? walk_list<1>(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out)
+                                    : walk_list<2>(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
+    if (uniform(cmax <= WALK_XGUARD)) {
+      *nhull = h;
+      return kg;
+    }
+  }
+  double la[MAXL], lb[MAXL];
+  build(la, lb);
+  return walk_regs<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bT, nhull, out);
+}
 
 // ---------------------------------------------------------------------------
 // Vertex visitors for the gradient: the envelope lines in increasing slope,
@@ -573,138 +589,6 @@ __device__ __forceinline__ double envelope_walk_stream(int nch, int nl, int lane
   return kg;
 }
 
-// Quickhull refinement of an overflowing survivor list (forward, streaming
-// envelope).  The list holds the cnt <= LIST_CAP_STREAM lines strictly above
-// chord L-T or T-R.  Known hull vertices V (slope order, in vb/va: L, T, R to
-// start) split the slope axis into chords; per chord the entry farthest above
-// it is itself an upper-hull vertex (it maximises a - (chord) at its slope over
-// that interval), so it joins V, and entries not strictly above the new chords
-// are dropped (collinear ones included: the reference walk skips them too,
-// discretekg.py:382-401 takes the larger slope on equal intersections).  Rounds
-// repeat until survivors + new vertices fit the hull stage; the new vertices
-// are then appended to the list (envelope_hull appends L, T, R itself).
-// Heights are h = (a - a_0)(b_1 - b_0) - (b - b_0)(a_1 - a_0), exactly 0 at
-// both chord ends.  Returns the new list length, or -1 (caller walks).
-__device__ __forceinline__ double vchord_h(double b, double a, const double* vb, const double* va, int c) {
-  const double b0 = vb[c], a0 = va[c], b1 = vb[c + 1], a1 = va[c + 1];
-  return (a - a0) * (b1 - b0) - (b - b0) * (a1 - a0);
-}
-
-// nv0 > 0: the vertex set (nv0 entries, T at tpos0) is already in vb/va
-// (refine_stream); otherwise it starts as L, T, R.
-__device__ __forceinline__ int refine_list(const EnvFilter& f, int cnt, int lane, double* sb, double* sa, double* vb,
-                                        double* va, int* vn, int nv0 = 0, int tpos0 = 1) {
-  constexpr int PL = LIST_CAP_STREAM / 64;
-  if (nv0 == 0 && lane == 0) {
-    vb[0] = f.bL; va[0] = f.aL;
-    vb[1] = f.bT; va[1] = f.aT;
-    vb[2] = f.bR; va[2] = f.aR;
-  }
-  int nv = nv0 ? nv0 : 3, tpos = nv0 ? tpos0 : 1;
-  for (int round = 0; round < 8; ++round) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (cnt + (nv - 3) <= ENV_CAP - 3) break;
-    if (nv >= VCAP / 2 + 1) return -1;  // a round may double the chords
-    double eb[PL], ea[PL], eh[PL];
-    int ec[PL];
-#pragma unroll
-    for (int q = 0; q < PL; ++q) {
-      const int e = min(lane + 64 * q, max(cnt - 1, 0));
-      eb[q] = sb[e];
-      ea[q] = sa[e];
-      int c = 0;
-      for (int i = 1; i < nv - 1; ++i) c += (eb[q] > vb[i]) ? 1 : 0;
-      ec[q] = c;
-      eh[q] = (lane + 64 * q < cnt) ? vchord_h(eb[q], ea[q], vb, va, c) : -1.0;
-    }
-    // farthest entry above each chord (wave argmax, ties -> lower list index);
-    // its list index goes to vn[chord] (lane 0), -1 when nothing is above
-    int found = 0;
-    uint64_t hasnew = 0;
-    for (int c = 0; c < nv - 1; ++c) {
-      double bh = 0.0;
-      int be = 1 << 30;
-#pragma unroll
-      for (int q = 0; q < PL; ++q) {
-        const bool take = ec[q] == c && eh[q] > bh;
-        bh = take ? eh[q] : bh;
-        be = take ? lane + 64 * q : be;
-      }
-      DKG_BUTTERFLY({
-        const double oh = partner_f64<S_>(bh);
-        const int oe = __shfl_xor(be, S_ == 0 ? 1 : S_ == 1 ? 2 : S_ == 2 ? 4 : S_ == 3 ? 8 : S_ == 4 ? 16 : 32);
-        const bool take = oh > bh || (oh == bh && oe < be);
-        bh = take ? oh : bh;
-        be = take ? oe : be;
-      })
-      const int e = __builtin_amdgcn_readfirstlane(be);
-      if (e < cnt) {  // wave-uniform: a line strictly above chord c
-        if (lane == 0) vn[c] = e;
-        hasnew |= 1ull << c;
-        ++found;
-      }
-    }
-    if (found == 0) return -1;  // cnt > 0 entries yet none above a chord: rounding; the caller walks
-    // new vertex set in slope order, built in place from the back by lane 0:
-    // old vertex i moves to i + (new vertices of chords < i); chord i's new
-    // vertex follows it.  Targets are >= sources, so no unread entry is overwritten.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) {
-      for (int i = nv - 1; i >= 0; --i) {
-        const int w = i + __popcll(hasnew & ((1ull << i) - 1));
-        const double b0 = vb[i], a0 = va[i];
-        if (i < nv - 1 && ((hasnew >> i) & 1)) {
-          const int e = vn[i];
-          vb[w + 1] = sb[e];
-          va[w + 1] = sa[e];
-        }
-        vb[w] = b0;
-        va[w] = a0;
-      }
-    }
-    tpos += __popcll(hasnew & ((1ull << tpos) - 1));
-    nv += found;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // re-filter against the new chords and compact in place (entries are in registers)
-    int nc = 0;
-#pragma unroll
-    for (int q = 0; q < PL; ++q) {
-      int c = 0;
-      for (int i = 1; i < nv - 1; ++i) c += (eb[q] > vb[i]) ? 1 : 0;
-      const bool keep = lane + 64 * q < cnt && vchord_h(eb[q], ea[q], vb, va, c) > 0.0;
-      const uint64_t mk = __ballot(keep);
-      if (keep) {
-        const int pos = nc + lanes_below(mk);
-        sb[pos] = eb[q];
-        sa[pos] = ea[q];
-      }
-      nc += __popcll(mk);
-    }
-    cnt = nc;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (cnt + (nv - 3) > ENV_CAP - 3) return -1;
-  // append the new vertices (every V entry but L, T, R)
-  if (lane == 0) {
-    int pos = cnt;
-    for (int i = 1; i < nv - 1; ++i) {
-      if (i == tpos) continue;
-      sb[pos] = vb[i];
-      sa[pos] = va[i];
-      ++pos;
-    }
-  }
-  return cnt + (nv - 3);
-}
-
 // Streaming quickhull round(s) for survivor lists longer than the LDS list
 // holds (cnt > LIST_CAP_STREAM): per chord of the known vertices V (L, T, R to
 // start), one pass over the streamed lines finds the farthest line strictly
@@ -735,13 +619,33 @@ __device__ __forceinline__ double chord_h_reg(double b, double a, const double (
   return (a - a0) * (b1 - b0) - (b - b0) * (a1 - a0);
 }
 
+// Margin form of the chord test (EnvChords): h >= -tau for the chord c the
+// line's slope falls in; a degenerate chord keeps only exact copies of its end.
+template <int NV>
+__device__ __forceinline__ bool chord_keep_reg(double b, double a, const double (&vb_)[NV], const double (&va_)[NV],
+                                               int c, double Wb) {
+  double b0 = vb_[0], a0 = va_[0], b1 = vb_[1], a1 = va_[1];
+#pragma unroll
+  for (int i = 1; i < NV - 1; ++i) {
+    const bool s = c == i;
+    b0 = s ? vb_[i] : b0;
+    a0 = s ? va_[i] : a0;
+    b1 = s ? vb_[i + 1] : b1;
+    a1 = s ? va_[i + 1] : a1;
+  }
+  const double db = b1 - b0, da = a1 - a0;
+  if (!(db > 0.0)) return b == b0 && a == a0;
+  const double tau = WALK_MARGIN * (fmax(fabs(a0), fabs(a1)) * db + fmax(fabs(b0), fabs(b1)) * fabs(da) + Wb * db);
+  return (a - a0) * db - (b - b0) * da >= -tau;
+}
+
 // One streaming round with NV = nv vertices (compile-time bound) read from LDS:
 // new vertices inserted into vb/va (lane 0), survivors of the 2(nv-1) chords
 // written to the list (capacity LIST_CAP_STREAM).  Returns the survivor count
 // (may exceed the capacity), or -1 if no line is above any chord.
 template <int MAXL, int NV, class Build>
-__device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* sb, double* sa, double* vb, double* va,
-                                            int& nv, int& tpos, Build&& build) {
+__device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* sb, double* sa, int* si, double* vb,
+                                            double* va, int& nv, int& tpos, Build&& build) {
   constexpr int NC = NV - 1;
   double vb_[NV], va_[NV];
 #pragma unroll
@@ -819,6 +723,7 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // pass B: survivors of the new chords into the list
   constexpr int NV2 = 2 * NV - 1;
+  const double Wb = vb[nv - 1] - vb[0];
   double wb_[NV2], wa_[NV2];
 #pragma unroll
   for (int i = 0; i < NV2; ++i) {
@@ -833,7 +738,7 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
     for (int t = 0; t < MAXL; ++t) {
       const int k = ch * 64 * MAXL + lane + 64 * t;
       const int c = chord_of<MAXL, NV2, Build>(lb[t], wb_, nv);
-      const bool keep = k < nl && chord_h_reg<NV2>(lb[t], la[t], wb_, wa_, c) > 0.0;
+      const bool keep = k < nl && chord_keep_reg<NV2>(lb[t], la[t], wb_, wa_, c, Wb);
       const uint64_t mk = __ballot(keep);
       if (mk != 0) {
         if (keep) {
@@ -841,6 +746,7 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
           if (pos < LIST_CAP_STREAM) {
             sb[pos] = lb[t];
             sa[pos] = la[t];
+            si[pos] = k;
           }
         }
         cnt += __popcll(mk);
@@ -851,8 +757,10 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
 }
 
 template <int MAXL, class Build>
-__device__ __forceinline__ int refine_stream(const EnvFilter& f, int nch, int nl, int lane, double* sb, double* sa,
-                                             double* vb, double* va, int* vn, Build&& build) {
+__device__ __forceinline__ int refine_stream(const FwdEnv& f, int nch, int nl, int lane, double* sb, double* sa,
+                                             int* si, double* vreg, Build&& build) {
+  double* vb = vreg;
+  double* va = vreg + VCAP;
   if (lane == 0) {
     vb[0] = f.bL; va[0] = f.aL;
     vb[1] = f.bT; va[1] = f.aT;
@@ -862,25 +770,139 @@ __device__ __forceinline__ int refine_stream(const EnvFilter& f, int nch, int nl
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   int nv = 3, tpos = 1;
-  int cnt = stream_round<MAXL, 3>(nch, nl, lane, sb, sa, vb, va, nv, tpos, build);
-  if (cnt > LIST_CAP_STREAM) cnt = stream_round<MAXL, 5>(nch, nl, lane, sb, sa, vb, va, nv, tpos, build);
-  if (cnt < 0 || cnt > LIST_CAP_STREAM) return -1;
-  return refine_list(f, cnt, lane, sb, sa, vb, va, vn, nv, tpos);
+  int cnt = stream_round<MAXL, 3>(nch, nl, lane, sb, sa, si, vb, va, nv, tpos, build);
+  if (cnt > LIST_CAP_STREAM) cnt = stream_round<MAXL, 5>(nch, nl, lane, sb, sa, si, vb, va, nv, tpos, build);
+  return (cnt < 0 || cnt > LIST_CAP_STREAM) ? -1 : cnt;
 }
 
-// Whole envelope stage for register-held lines (lines_kg_kernel).
-template <int MAXL>
-__device__ __forceinline__ double envelope_kg(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
-                                              double* sb, double* sa, int* nhull) {
-  const EnvFilter f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
+// Streaming forward (line sets too large for registers / LDS staging): the
+// extremes in one lexicographic pass over the streamed lines, the margin
+// filter into the wave's long list (LIST_CAP_STREAM entries), streamed
+// quickhull rounds when that overflows, then the walk over the list.
+template <int MAXL, class Build>
+__device__ __forceinline__ FwdEnv env_extremes_stream(int nch, int nl, int lane, Build&& build) {
+  FwdEnv f;
+  double bmin = INFINITY, aLx = -INFINITY, bmax = -INFINITY, aRx = -INFINITY, amax = -INFINITY, bTx = INFINITY;
+  for (int c = 0; c < nch; ++c) {
+    double la[MAXL], lb[MAXL];
+    build(c, la, lb);
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const bool live = c * 64 * MAXL + lane + 64 * t < nl;
+      const double a = la[t], b = lb[t];
+      const bool l = live && (b < bmin || (b == bmin && a > aLx));
+      bmin = l ? b : bmin;
+      aLx = l ? a : aLx;
+      const bool r = live && (b > bmax || (b == bmax && a > aRx));
+      bmax = r ? b : bmax;
+      aRx = r ? a : aRx;
+      const bool tt = live && (a > amax || (a == amax && b < bTx));
+      amax = tt ? a : amax;
+      bTx = tt ? b : bTx;
+    }
+  }
+  DKG_BUTTERFLY({
+    const double ob = partner_f64<S_>(bmin), oa = partner_f64<S_>(aLx);
+    const bool l = ob < bmin || (ob == bmin && oa > aLx);
+    bmin = l ? ob : bmin;
+    aLx = l ? oa : aLx;
+    const double ob2 = partner_f64<S_>(bmax), oa2 = partner_f64<S_>(aRx);
+    const bool r = ob2 > bmax || (ob2 == bmax && oa2 > aRx);
+    bmax = r ? ob2 : bmax;
+    aRx = r ? oa2 : aRx;
+    const double oa3 = partner_f64<S_>(amax), ob3 = partner_f64<S_>(bTx);
+    const bool tt = oa3 > amax || (oa3 == amax && ob3 < bTx);
+    amax = tt ? oa3 : amax;
+    bTx = tt ? ob3 : bTx;
+  })
+  f.bL = bmin; f.aL = aLx; f.bR = bmax; f.aR = aRx; f.aT = amax; f.bT = bTx;
+  f.cnt = 0;
+  f.status = uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax) ? 0 : 1;
+  return f;
+}
+
+template <int MAXL, class Build>
+__device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, double* sb, double* sa, int* si,
+                                                  double* vreg, bool force_walk, int* nhull, Build&& build) {
+  const FwdEnv f = env_extremes_stream<MAXL>(nch, nl, lane, build);
   if (f.status == 1) {
-    if (nhull) *nhull = 1;
+    *nhull = 1;
     return 0.0;
   }
-  if (f.status == 2) return envelope_walk<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bR, f.bT, nhull);
-  return envelope_hull(f, lane, sb, sa, nhull);
+  const EnvChords ch = env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR);
+  int cnt = 0;
+  for (int c = 0; c < nch; ++c) {
+    double la[MAXL], lb[MAXL];
+    build(c, la, lb);
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const int k = c * 64 * MAXL + lane + 64 * t;
+      const bool s = k < nl && env_keep(ch, la[t], lb[t]);
+      const uint64_t mk = __ballot(s);
+      if (mk != 0) {
+        if (s) {
+          const int pos = cnt + lanes_below(mk);
+          if (pos < LIST_CAP_STREAM) {
+            sb[pos] = lb[t];
+            sa[pos] = la[t];
+            si[pos] = k;
+          }
+        }
+        cnt += __popcll(mk);
+      }
+    }
+  }
+  if (cnt > LIST_CAP_STREAM && !force_walk) cnt = refine_stream<MAXL>(f, nch, nl, lane, sb, sa, si, vreg, build);
+  if (cnt >= 0 && cnt <= LIST_CAP_STREAM && !force_walk) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double cmax, kg;
+    int h;
+    if (cnt <= 64) kg = walk_list<1>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
+    else if (cnt <= 128) kg = walk_list<2>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
+    else if (cnt <= 256) kg = walk_list<4>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
+    else kg = walk_list<8>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
+    if (uniform(cmax <= WALK_XGUARD)) {
+      *nhull = h;
+      return kg;
+    }
+  }
+  return walk_stream<MAXL>(nch, nl, lane, f.bL, f.aL, f.bT, nhull, build);
 }
 
+// Line coefficients of one (candidate, scalarisation) pair (discretekg.py:
+// 182-223 full, :300-321 decoupled), wave-uniform: a_k = a_off + sum_i wa_i
+// mu_i(z_k), b_k = sum_i wb_i cov_i(x_b, z_k); den = the scalarised noisy
+// variance under the square root.  Outputs i >= m carry zero weights.  One
+// definition for envelope_kernel and lines_export_kernel, so the exported
+// lines are the envelope's lines bit for bit.
+template <int M>
+__device__ __forceinline__ void pair_coefs(const double* wrow, int m, bool full, int target, const double (&ysd)[M],
+                                           const double (&ymu)[M], const double (&nz)[M], const double (&sv)[M],
+                                           double (&w)[M], double (&wa)[M], double (&wb)[M], double& a_off,
+                                           double& den) {
+  a_off = 0.0;
+  den = 0.0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    w[i] = (i < m) ? wrow[i] : 0.0;
+    wa[i] = w[i] * ysd[i];
+    a_off = fma(w[i], ymu[i], a_off);
+    den = fma(w[i] * w[i], ysd[i] * ysd[i] * (sv[i] + nz[i]), den);
+  }
+  if (full) {
+    const double inv_den = 1.0 / sqrt(den);
+#pragma unroll
+    for (int i = 0; i < M; ++i) wb[i] = w[i] * w[i] * ysd[i] * ysd[i] * inv_den;
+  } else {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const double sd2 = ysd[i] * ysd[i];
+      wb[i] = (i == target) ? w[i] * sd2 / sqrt(sd2 * (sv[i] + nz[i])) : 0.0;
+    }
+  }
+}
 
 // Padded length (doubles) of one LDS-staged line array: whole 1 KiB DMA pieces.
 __host__ __device__ inline int stage_len(int N) { return ((N + 127) / 128) * 128; }
@@ -1117,6 +1139,9 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   double* sa = sb + LC;
   // streaming forward: the quickhull refinement's vertex arrays after the lists
   double* vreg = sbuf + (size_t)SW * 2 * LC + (size_t)wave * VREG;
+  // forward: the list's line indices after the vertex arrays (GRAD: sidx)
+  int* sif = reinterpret_cast<int*>(sbuf + (size_t)SW * (2 * LC + ((STREAM && !GRAD) ? VREG : 0))) +
+             (size_t)wave * LC;
   double wave_acc = 0.0;
   int* si = nullptr;
   double* gw = nullptr;
@@ -1149,27 +1174,10 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
 
   for (int j = g * SW + wave; j < S; j += waves_total) {
-    // ---- line coefficients (wave uniform)
+    // ---- line coefficients (wave uniform; shared with lines_export_kernel)
     double w[M], wa[M], wb[M];
-    double a_off = 0.0, den = 0.0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      w[i] = (i < m) ? lw[j * m + i] : 0.0;
-      wa[i] = w[i] * ysd[i];
-      a_off = fma(w[i], ymu[i], a_off);
-      den = fma(w[i] * w[i], ysd[i] * ysd[i] * (sv[i] + nz[i]), den);
-    }
-    if (full) {
-      const double inv_den = 1.0 / sqrt(den);
-#pragma unroll
-      for (int i = 0; i < M; ++i) wb[i] = w[i] * w[i] * ysd[i] * ysd[i] * inv_den;
-    } else {
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const double sd2 = ysd[i] * ysd[i];
-        wb[i] = (i == target) ? w[i] * sd2 / sqrt(sd2 * (sv[i] + nz[i])) : 0.0;
-      }
-    }
+    double a_off, den;
+    pair_coefs<M>(lw + j * m, m, full, target, ysd, ymu, nz, sv, w, wa, wb, a_off, den);
     // ---- lines: slot t of lane l is line k = l + 64 t (k = 0: the candidate).
     // Branch-free bodies (one LDS read stream per array, no per-slot waits):
     // unused output slots read output 0 with a zero weight.  Rebuilt from the
@@ -1260,8 +1268,8 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
 
     double kgj;
     int hn = 1;  // upper-envelope lines of this pair (recorded with kg_pairs)
-    EnvFilter f;
     if constexpr (GRAD) {
+      EnvFilter f;
       if constexpr (STREAM) {
         f = envelope_filter_stream<MAXL, true>(nch, lane, sb, sa, si, build_chunk);
       } else {
@@ -1513,39 +1521,12 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       if (lane == 0)
         for (int dd = 0; dd < d; ++dd) gw[dd] = 0.0;
     } else if constexpr (STREAM) {
-      f = envelope_filter_stream<MAXL, false, LC>(nch, lane, sb, sa, nullptr, build_chunk);
-      if (force_walk && f.status == 0) f.status = 2;
-      if (f.status == 2 && !force_walk) {
-        // too many survivors for the hull stage: quickhull rounds (on the streamed lines while the
-        // list overflows its LDS capacity, then on the list), not a walk over the lines per vertex
-        int* vn = reinterpret_cast<int*>(vreg + 2 * VCAP);
-        const int nc = (f.cnt <= LC) ? refine_list(f, f.cnt, lane, sb, sa, vreg, vreg + VCAP, vn)
-                                     : refine_stream<MAXL>(f, nch, NL, lane, sb, sa, vreg, vreg + VCAP, vn,
-                                                           build_chunk);
-        if (nc >= 0) {
-          f.cnt = nc;
-          f.status = 0;
-        }
-      }
+      kgj = env_pair_stream<MAXL>(nch, NL, lane, sb, sa, sif, vreg, force_walk, &hn, build_chunk);
     } else {
-      double la[MAXL], lb[MAXL];
-      build_lines(la, lb);
-      f = envelope_filter<MAXL>(la, lb, lane, sb, sa);
-      if (force_walk && f.status == 0) f.status = 2;
-    }
-    if constexpr (GRAD) {
-    } else if (f.status == 1) {
-      kgj = 0.0;
-    } else if (f.status == 0) {
-      kgj = envelope_hull(f, lane, sb, sa, &hn);
-    } else if constexpr (STREAM) {  // list overflow: gift wrap over the streamed lines
-      auto count_visit = [&](int, double, double, double, double) { ++hn; };
-      hn = 0;
-      kgj = envelope_walk_stream<MAXL>(nch, NL, lane, f, build_chunk, count_visit, -1);
-    } else {  // list overflow: gift wrap over the (rebuilt) register lines
-      double la[MAXL], lb[MAXL];
-      build_lines(la, lb);
-      kgj = envelope_walk<MAXL>(la, lb, NL, lane, f.bL, f.aL, f.bR, f.bT, &hn);
+      // the lines are rebuilt from the staged LDS data if the list walk cannot finish,
+      // so no register line is live across it
+      auto rebuild = [&](double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
+      kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn);
     }
     if (pairs_out != nullptr && lane == 0) {
       pairs_out[(size_t)b * S + j] = kgj;
@@ -1594,6 +1575,59 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
   __syncthreads();
   KST_END(st);
+}
+
+// The lines of every (candidate, scalarisation) pair of the plan's last
+// cross / covariance stages, as the envelope builds them (dkg_plan_lines):
+// a_out / b_out [B][S][N + 1], line 0 the candidate itself.  Grid (B, S).
+template <int M>
+__global__ __launch_bounds__(256) void lines_export_kernel(const Plan* __restrict__ P, double* __restrict__ a_out,
+                                                            double* __restrict__ b_out) {
+  const int b = blockIdx.x, j = blockIdx.y;
+  const int m = P->m, N = P->N, S = P->S, target = P->target, bpad = P->bpad;
+  const bool full = target < 0;
+  double sv[M], mx0[M], ysd[M], ymu[M], nz[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const bool live = i < m;
+    ysd[i] = live ? P->o[i].y_std : 1.0;
+    ymu[i] = live ? P->o[i].y_mean : 0.0;
+    nz[i] = live ? P->o[i].noise : 0.0;
+    sv[i] = live ? P->var_all[(size_t)i * bpad + b] : 0.0;
+    mx0[i] = live ? P->mux_all[(size_t)i * bpad + b] : 0.0;
+  }
+  double w[M], wa[M], wb[M];
+  double a_off, den;
+  pair_coefs<M>(P->weights + (size_t)j * m, m, full, target, ysd, ymu, nz, sv, w, wa, wb, a_off, den);
+  (void)den;
+  double* ao = a_out + ((size_t)b * S + j) * (N + 1);
+  double* bo = b_out + ((size_t)b * S + j) * (N + 1);
+  for (int k = threadIdx.x; k <= N; k += blockDim.x) {
+    double a = a_off, bb = 0.0;
+    if (k == 0) {
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        a = fma(wa[i], mx0[i], a);
+        bb = fma(wb[i], sv[i], bb);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (i < m) {
+          a = fma(wa[i], P->mu_all[(size_t)i * N + k - 1], a);
+          if (full) bb = fma(wb[i], P->cov_all[(size_t)i * P->cov_stride + (size_t)b * N + k - 1], bb);
+        }
+      }
+      if (!full) {
+        double wbt = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
+        bb = wbt * P->cov_all[(size_t)target * P->cov_stride + (size_t)b * N + k - 1];
+      }
+    }
+    ao[k] = a;
+    bo[k] = bb;
+  }
 }
 
 struct EnvLaunch {

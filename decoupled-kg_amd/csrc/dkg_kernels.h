@@ -77,7 +77,15 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
                         hipStream_t s, int stage);
 hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                           hipStream_t s, hipEvent_t* ev);
-hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s);
+// Envelope stage alone over P sets of L lines: KG, envelope sizes (nullable) and, when idx is given, the
+// reference walk's indices [P][cap] and intersections [P][cap - 1] (lines_kg_kernel / lines_walk_kernel).
+hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, long long* idx,
+                           double* xs, int cap, hipStream_t s);
+// The lines of every (candidate, scalarisation) pair after stages 0-1 (dkg_plan_lines).
+hipError_t launch_lines_export(const Plan& h, const Plan* dev, int B, double* a_out, double* b_out, hipStream_t s);
+// Reference formula of E[f(Z)] for P piecewise-linear f of m pieces (dkg_pwl_expectation).
+hipError_t launch_pwl_expectation(const double* a, const double* b, const double* c, int P, int m, double* out,
+                                  hipStream_t s);
 // Per-workgroup phase stamps of the forward kernels: [3 kernels][KST_WG][8].
 constexpr int KST_WG = 1024;
 hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s);

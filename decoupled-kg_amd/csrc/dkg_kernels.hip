@@ -477,8 +477,10 @@ size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad
   const int M = outputs_bucket(m);
   const size_t staged = stream ? 0 : 2 * (size_t)M * stage_stride(N);
   const bool refine = stream && !grad;  // streaming forward: long lists + quickhull vertex arrays
-  return ((size_t)2 + staged + ((S * m + 1) & ~1) + (size_t)waves * 2 * list_cap(refine) +
-          (refine ? (size_t)waves * VREG : 0)) * sizeof(double);
+  const size_t lc = list_cap(refine);
+  // per wave: the list (slopes, intercepts; forward: line indices) and the streaming vertex arrays
+  return ((size_t)2 + staged + ((S * m + 1) & ~1) + (size_t)waves * 2 * lc + (refine ? (size_t)waves * VREG : 0) +
+          (grad ? 0 : ((size_t)waves * lc + 1) / 2)) * sizeof(double);
 }
 
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream) {
@@ -494,28 +496,89 @@ size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np
 // ---------------------------------------------------------------------------
 // lines_kg_kernel: KG = E[max_k (a_k + b_k Z)] - max_k a_k for P independent
 // sets of L lines (row-major [P][L]); one wave per set.  Exposes the envelope
-// stage on its own (reference calculate_epigraph_indices +
-// calculate_expected_value_of_piecewise_linear_function, discretekg.py:341-452).
+// stage on its own: the reference walk (calculate_epigraph_indices,
+// discretekg.py:341-412, exactly: dkg_walk.h) and the cancellation-free
+// expectation (calculate_expected_value_of_piecewise_linear_function + the
+// baseline, :225-233, 415-452).  idx / xs (nullable): the walk's line indices
+// [P][cap] and intersections [P][cap - 1] (dkg_epigraph).
 template <int MAXL>
 __global__ __launch_bounds__(256) void lines_kg_kernel(const double* __restrict__ a, const double* __restrict__ b,
-                                                        int P, int L, double* __restrict__ kg, int* __restrict__ nhull) {
+                                                        int P, int L, double* __restrict__ kg, int* __restrict__ nhull,
+                                                        long long* __restrict__ idx, double* __restrict__ xs,
+                                                        int cap) {
   extern __shared__ __attribute__((aligned(16))) double sbuf[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p = blockIdx.x * (blockDim.x >> 6) + wave;
   if (p >= P) return;
-  double la[MAXL], lb[MAXL];
+  // line k >= L: a NaN intercept (never an extreme, a survivor or a successor)
+  auto build = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
 #pragma unroll
-  for (int t = 0; t < MAXL; ++t) {
-    const int k = min(lane + 64 * t, L - 1);
-    la[t] = a[(size_t)p * L + k];
-    lb[t] = b[(size_t)p * L + k];
-  }
+    for (int t = 0; t < MAXL; ++t) {
+      const int k = lane + 64 * t;
+      const int kk = min(k, L - 1);
+      la[t] = (k < L) ? a[(size_t)p * L + kk] : __builtin_nan("");
+      lb[t] = b[(size_t)p * L + kk];
+    }
+  };
+  const int nw = blockDim.x >> 6;
   double* sb = sbuf + (size_t)wave * 2 * ENV_CAP;
+  int* si = reinterpret_cast<int*>(sbuf + (size_t)nw * 2 * ENV_CAP) + (size_t)wave * ENV_CAP;
+  WalkOut out{idx ? idx + (size_t)p * cap : nullptr, xs ? xs + (size_t)p * (cap > 1 ? cap - 1 : 1) : nullptr, cap};
   int h = 0;
-  const double v = envelope_kg<MAXL>(la, lb, L, lane, sb, sb + ENV_CAP, &h);
+  const double v = env_pair_regs<MAXL>(build, L, lane, sb, sb + ENV_CAP, si, false, &h, idx ? &out : nullptr);
   if (lane == 0) {
-    kg[p] = v;
+    if (kg) kg[p] = v;
+    if (nhull) nhull[p] = h;
+  }
+}
+
+// Epigraph of line sets too long for the register path (L > 64 * 33): the
+// reference walk over all lines, streamed from global memory each step.
+__global__ __launch_bounds__(256) void lines_walk_kernel(const double* __restrict__ a, const double* __restrict__ b,
+                                                         int P, int L, double* __restrict__ kg,
+                                                         int* __restrict__ nhull, long long* __restrict__ idx,
+                                                         double* __restrict__ xs, int cap) {
+  constexpr int MAXL = 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (p >= P) return;
+  const double* ap = a + (size_t)p * L;
+  const double* bp = b + (size_t)p * L;
+  auto build = [&](int c, double (&la)[MAXL], double (&lb)[MAXL]) {
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const int k = min(c * 64 * MAXL + lane + 64 * t, L - 1);
+      la[t] = ap[k];
+      lb[t] = bp[k];
+    }
+  };
+  const int nch = (L + 64 * MAXL - 1) / (64 * MAXL);
+  const FwdEnv f = env_extremes_stream<MAXL>(nch, L, lane, build);
+  WalkOut out{idx ? idx + (size_t)p * cap : nullptr, xs ? xs + (size_t)p * (cap > 1 ? cap - 1 : 1) : nullptr, cap};
+  int h = 1;
+  double v = 0.0;
+  if (f.status == 1) {
+    if (idx && cap > 0) {  // first line attaining max a
+      int k = KEY_NONE;
+      for (int c = nch - 1; c >= 0; --c) {
+        double la[MAXL], lb[MAXL];
+        build(c, la, lb);
+#pragma unroll
+        for (int t = MAXL - 1; t >= 0; --t) {
+          const int kk = c * 64 * MAXL + lane + 64 * t;
+          k = (kk < L && la[t] == f.aT) ? kk : k;
+        }
+      }
+      k = wave_min_i32(k);
+      if (lane == 0) out.idx[0] = k;
+    }
+  } else {
+    v = walk_stream<MAXL>(nch, L, lane, f.bL, f.aL, f.bT, &h, build, idx ? &out : nullptr);
+  }
+  if (lane == 0) {
+    if (kg) kg[p] = v;
     if (nhull) nhull[p] = h;
   }
 }
@@ -699,19 +762,63 @@ hipError_t launch_forward(const Plan& h, const Plan* dev, const double* xnew, in
   return hipSuccess;
 }
 
-hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, hipStream_t s) {
+hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, long long* idx,
+                           double* xs, int cap, hipStream_t s) {
   const int wpb = 4;
   dim3 grid((P + wpb - 1) / wpb), block(wpb * WAVE);
-  const size_t lds = (size_t)wpb * 2 * ENV_CAP * sizeof(double);
-  if (L <= 64 * 2) hipLaunchKernelGGL(lines_kg_kernel<2>, grid, block, lds, s, a, b, P, L, kg, nhull);
-  else if (L <= 64 * 4) hipLaunchKernelGGL(lines_kg_kernel<4>, grid, block, lds, s, a, b, P, L, kg, nhull);
-  else if (L <= 64 * 8) hipLaunchKernelGGL(lines_kg_kernel<8>, grid, block, lds, s, a, b, P, L, kg, nhull);
-  else if (L <= 64 * 17) hipLaunchKernelGGL(lines_kg_kernel<17>, grid, block, lds, s, a, b, P, L, kg, nhull);
-  else if (L <= 64 * 33) hipLaunchKernelGGL(lines_kg_kernel<33>, grid, block, lds, s, a, b, P, L, kg, nhull);
-  else return hipErrorInvalidValue;
+  const size_t lds = (size_t)wpb * 2 * ENV_CAP * sizeof(double) + (size_t)wpb * ENV_CAP * sizeof(int);
+  if (L <= 64 * 2) hipLaunchKernelGGL(lines_kg_kernel<2>, grid, block, lds, s, a, b, P, L, kg, nhull, idx, xs, cap);
+  else if (L <= 64 * 4) hipLaunchKernelGGL(lines_kg_kernel<4>, grid, block, lds, s, a, b, P, L, kg, nhull, idx, xs, cap);
+  else if (L <= 64 * 8) hipLaunchKernelGGL(lines_kg_kernel<8>, grid, block, lds, s, a, b, P, L, kg, nhull, idx, xs, cap);
+  else if (L <= 64 * 17) hipLaunchKernelGGL(lines_kg_kernel<17>, grid, block, lds, s, a, b, P, L, kg, nhull, idx, xs, cap);
+  else if (L <= 64 * 33) hipLaunchKernelGGL(lines_kg_kernel<33>, grid, block, lds, s, a, b, P, L, kg, nhull, idx, xs, cap);
+  else hipLaunchKernelGGL(lines_walk_kernel, grid, block, 0, s, a, b, P, L, kg, nhull, idx, xs, cap);
   return hipGetLastError();
 }
 
+hipError_t launch_lines_export(const Plan& h, const Plan* dev, int B, double* a_out, double* b_out, hipStream_t s) {
+  const dim3 grid(B, h.S), block(256);
+  switch (outputs_bucket(h.m)) {
+    case 1: hipLaunchKernelGGL(lines_export_kernel<1>, grid, block, 0, s, dev, a_out, b_out); break;
+    case 2: hipLaunchKernelGGL(lines_export_kernel<2>, grid, block, 0, s, dev, a_out, b_out); break;
+    case 3: hipLaunchKernelGGL(lines_export_kernel<3>, grid, block, 0, s, dev, a_out, b_out); break;
+    case 4: hipLaunchKernelGGL(lines_export_kernel<4>, grid, block, 0, s, dev, a_out, b_out); break;
+    default: hipLaunchKernelGGL(lines_export_kernel<8>, grid, block, 0, s, dev, a_out, b_out); break;
+  }
+  return hipGetLastError();
+}
+
+// E[f(Z)] of a piecewise-linear f given its pieces and boundaries, the
+// reference's formula (calculate_expected_value_of_piecewise_linear_function,
+// discretekg.py:415-452): sum_j a_j (Phi(c_j+1) - Phi(c_j)) - b_j (phi(c_j+1) - phi(c_j)),
+// c_0 = -inf, c_m = +inf, with torch's Normal: pdf = exp(log_prob), cdf = (1 + erf(z / sqrt 2)) / 2.
+// One wave per set of m pieces.
+__global__ __launch_bounds__(256) void pwl_expectation_kernel(const double* __restrict__ a, const double* __restrict__ b,
+                                                              const double* __restrict__ c, int P, int m,
+                                                              double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (p >= P) return;
+  auto bound = [&](int j) {  // c_j, j = 0 .. m
+    return j == 0 ? -INFINITY : j == m ? INFINITY : c[(size_t)p * (m - 1) + j - 1];
+  };
+  auto pdf = [](double z) { return exp(-0.5 * z * z - 0.91893853320467274178); };  // log(sqrt(2 pi))
+  auto cdf = [](double z) { return 0.5 * (1.0 + erf(z * 0.70710678118654752440)); };
+  double acc = 0.0;
+  for (int j = lane; j < m; j += 64) {
+    const double lo = bound(j), hi = bound(j + 1);
+    acc += a[(size_t)p * m + j] * (cdf(hi) - cdf(lo)) - b[(size_t)p * m + j] * (pdf(hi) - pdf(lo));
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) out[p] = acc;
+}
+
+hipError_t launch_pwl_expectation(const double* a, const double* b, const double* c, int P, int m, double* out,
+                                  hipStream_t s) {
+  const int wpb = 4;
+  hipLaunchKernelGGL(pwl_expectation_kernel, dim3((P + wpb - 1) / wpb), dim3(wpb * WAVE), 0, s, a, b, c, P, m, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s) {
   hipLaunchKernelGGL(debug_wave_kernel, dim3(1), dim3(64), 0, s, in, out);

@@ -1,0 +1,288 @@
+// The reference's epigraph walk, exactly (calculate_epigraph_indices,
+// discretekg.py:341-412), as wave-level device code for gfx950.
+//
+// The reference sorts the lines by slope ascending, then intercept descending
+// (:370-374), starts from the first line and repeatedly jumps to the later
+// line with a different slope whose intersection
+//     x = -(a_cur - a_j) / (b_cur - b_j)                           (:388-396)
+// comes first; torch.argmin takes the first index among equal x, i.e. the
+// smallest slope, then the largest intercept, then (sorts taken stable) the
+// smallest line index.  Here a step is an argmin over the candidate lines of
+// the key (x, b, -a, k), with x computed by the same IEEE operations: the
+// numerator a_cur - a_j and the denominator b_j - b_cur are the reference's
+// operands up to sign (exact), and the division is correctly rounded, so x is
+// bit-identical to the reference's and the walk visits the same lines in the
+// same order — concurrent lines at a breakpoint included (a zero-length
+// envelope segment in exact arithmetic, kept by the reference's argmin-first
+// rule).
+//
+// The walk runs over a candidate list rather than all N+1 lines: the lines on
+// or above the chords L-T and T-R less a margin (EnvChords).  A line below a
+// chord by more than the margin is below the upper hull by at least as much;
+// it can win a rounded argmin step only where the step's intersection exceeds
+// WALK_XGUARD in magnitude (derivation in DESIGN.md 4.3), so a walk whose
+// breakpoints all stay within WALK_XGUARD is the reference's walk over all
+// lines.  A walk that leaves it is redone over all lines (walk_regs /
+// walk_stream), as is a list that overflows.
+#pragma once
+
+#include "dkg_common.h"
+
+namespace dkg {
+
+constexpr int KEY_NONE = 0x7fffffff;
+// Relative chord margin 2^-30 (EnvChords) and the breakpoint bound under which
+// the list walk is provably the full walk: 2^20 < 2^23 / 6.
+constexpr double WALK_MARGIN = 9.313225746154785e-10;  // 2^-30
+constexpr double WALK_XGUARD = 1048576.0;              // 2^20
+
+// psi(c) = E[(Z - c)_+] with the far tail cut to its fp64 value (0 beyond
+// c = 40: exp(-800) underflows), so an infinite breakpoint gives 0, not NaN.
+__device__ __forceinline__ double psi_edge(double c) { return c > 40.0 ? 0.0 : psi(c); }
+
+// Walk order of candidate successors: intersection, then the reference's sort
+// order (slope ascending, intercept descending, index ascending).
+__device__ __forceinline__ bool walk_less(double x1, double b1, double a1, int k1, double x2, double b2, double a2,
+                                          int k2) {
+  return x1 < x2 || (x1 == x2 && (b1 < b2 || (b1 == b2 && (a1 > a2 || (a1 == a2 && k1 < k2)))));
+}
+
+struct WalkPick {
+  double x, b, a;
+  int k;
+};
+
+// Wave argmin of the walk key; lanes without a candidate hold
+// (+inf, +inf, -inf, KEY_NONE), which every candidate beats.  The common case
+// is one lane at the minimal x; ties fall through to the sort keys.
+__device__ __forceinline__ WalkPick wave_walk_min(double x, double b, double a, int k) {
+  double xm = x;
+  DKG_BUTTERFLY_ROW({ xm = fmin_raw(xm, partner_f64<S_>(xm)); })
+  xm = combine_rows(xm, [](double p, double q) { return fmin(p, q); });
+  const uint64_t tie = __ballot(x == xm);
+  WalkPick r;
+  r.x = xm;
+  if (__popcll(tie) == 1) {
+    const int w = __builtin_ctzll(tie);
+    r.b = readlane_f64(b, w);
+    r.a = readlane_f64(a, w);
+    r.k = __builtin_amdgcn_readlane(k, w);
+    return r;
+  }
+  const bool t0 = x == xm;
+  double bm = t0 ? b : INFINITY;
+  DKG_BUTTERFLY_ROW({ bm = fmin_raw(bm, partner_f64<S_>(bm)); })
+  bm = combine_rows(bm, [](double p, double q) { return fmin(p, q); });
+  const bool t1 = t0 && b == bm;
+  double am = t1 ? a : -INFINITY;
+  DKG_BUTTERFLY_ROW({ am = fmax_raw(am, partner_f64<S_>(am)); })
+  am = combine_rows(am, [](double p, double q) { return fmax(p, q); });
+  const bool t2 = t1 && a == am;
+  r.b = bm;
+  r.a = am;
+  r.k = wave_min_i32(t2 ? k : KEY_NONE);
+  return r;
+}
+
+// Optional per-pair epigraph output (dkg_epigraph): indices [cap] (left to
+// right) and intersections [cap - 1]; entries beyond cap are counted, not written.
+struct WalkOut {
+  long long* idx;
+  double* x;
+  int cap;
+};
+
+// Per-step bookkeeping shared by the walks: the KG edge terms
+// (b_Q - b_P) psi(+-c) (minus sign for edges ending at or left of T), one
+// edge per lane, flushed by a wave sum every 64 steps; the largest |c|; and
+// the optional epigraph output.
+struct WalkAcc {
+  double ec = 0.0, ed = 0.0, kg = 0.0, cmax = 0.0;
+  int h = 0;  // steps taken (envelope lines - 1)
+
+  __device__ __forceinline__ void start(int k0, int lane, const WalkOut* out) {
+    if (out && lane == 0 && out->cap > 0) out->idx[0] = k0;
+  }
+  __device__ __forceinline__ void step(const WalkPick& p, double bc, double bT, int lane, const WalkOut* out) {
+    if (lane == (h & 63)) {
+      ec = (p.b <= bT) ? -p.x : p.x;
+      ed = p.b - bc;
+    }
+    cmax = fmax(cmax, fabs(p.x));
+    if (out && lane == 0 && h + 1 < out->cap) {
+      out->idx[h + 1] = p.k;
+      out->x[h] = p.x;
+    }
+    ++h;
+    if ((h & 63) == 0) {
+      kg += wave_sum(ed * psi_edge(ec));
+      ec = 0.0;
+      ed = 0.0;
+    }
+  }
+  __device__ __forceinline__ double finish(int lane) {
+    if (h & 63) kg += wave_sum(lane < (h & 63) ? ed * psi_edge(ec) : 0.0);
+    return kg;
+  }
+};
+
+// Chords L-T and T-R of the candidate filter with the margin: a line (a, b)
+// is kept iff fma(a, db, -(b da)) >= k for either chord, where
+// k = fma(a0, db, -(b0 da)) - tau, tau = 2^-30 (max|a_end| db + max|b_end| |da| + (b_R - b_L) db):
+// the margin is at least 2^-30 (b_R - b_L) in intercept units at the line's
+// slope.  Exact copies of the chord ends evaluate to k + tau, so L, T, R and
+// their duplicates are always kept.  A degenerate chord (db = 0, then da = 0)
+// keeps nothing.
+struct EnvChords {
+  double db1, da1, k1, db2, da2, k2;
+};
+
+__device__ __forceinline__ EnvChords env_chords(double bL, double aL, double bT, double aT, double bR, double aR) {
+  EnvChords c;
+  const double Wb = bR - bL;
+  c.db1 = bT - bL;
+  c.da1 = aT - aL;
+  c.db2 = bR - bT;
+  c.da2 = aR - aT;
+  const double t1 = WALK_MARGIN * (fmax(fabs(aL), fabs(aT)) * c.db1 + fmax(fabs(bL), fabs(bT)) * fabs(c.da1) + Wb * c.db1);
+  const double t2 = WALK_MARGIN * (fmax(fabs(aT), fabs(aR)) * c.db2 + fmax(fabs(bT), fabs(bR)) * fabs(c.da2) + Wb * c.db2);
+  c.k1 = (c.db1 > 0.0) ? fma(aL, c.db1, -(bL * c.da1)) - t1 : INFINITY;
+  c.k2 = (c.db2 > 0.0) ? fma(aT, c.db2, -(bT * c.da2)) - t2 : INFINITY;
+  return c;
+}
+
+__device__ __forceinline__ bool env_keep(const EnvChords& c, double a, double b) {
+  return fma(a, c.db1, -(b * c.da1)) >= c.k1 || fma(a, c.db2, -(b * c.da2)) >= c.k2;
+}
+
+// Exact walk over the candidate list (sb, sa, si; nc <= 64 PL entries) from
+// the lowest-index copy of L = (bL, aL).  Returns KG_w (cancellation-free edge
+// sum); *nhull = envelope lines; *cmax = largest |breakpoint| (the caller
+// checks it against WALK_XGUARD).
+template <int PL>
+__device__ __forceinline__ double walk_list(int nc, int lane, const double* sb, const double* sa, const int* si,
+                                            double bL, double aL, double bT, int* nhull, double* cmax,
+                                            const WalkOut* out = nullptr) {
+  double eb[PL], ea[PL];
+  int ek[PL];
+#pragma unroll
+  for (int q = 0; q < PL; ++q) {
+    const int e = lane + 64 * q;
+    const int ee = min(e, max(nc - 1, 0));
+    const bool v = e < nc;
+    eb[q] = v ? sb[ee] : -INFINITY;  // never a successor, never the start
+    ea[q] = sa[ee];
+    ek[q] = v ? si[ee] : KEY_NONE;
+  }
+  int ks = KEY_NONE;
+#pragma unroll
+  for (int q = 0; q < PL; ++q) ks = (eb[q] == bL && ea[q] == aL) ? min(ks, ek[q]) : ks;
+  ks = wave_min_i32(ks);
+  WalkAcc acc;
+  acc.start(ks, lane, out);
+  double bc = bL, ac = aL;
+  for (int guard = 0; guard < nc; ++guard) {
+    double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
+    int kb = KEY_NONE;
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+      if (eb[q] > bc) {
+        const double x = (ac - ea[q]) / (eb[q] - bc);
+        if (walk_less(x, eb[q], ea[q], ek[q], xb, bb, ab, kb)) {
+          xb = x; bb = eb[q]; ab = ea[q]; kb = ek[q];
+        }
+      }
+    }
+    if (__ballot(kb != KEY_NONE) == 0) break;
+    const WalkPick p = wave_walk_min(xb, bb, ab, kb);
+    acc.step(p, bc, bT, lane, out);
+    bc = p.b;
+    ac = p.a;
+  }
+  *nhull = acc.h + 1;
+  *cmax = acc.cmax;
+  return acc.finish(lane);
+}
+
+// Exact walk over all register lines (line k = lane + 64 t, k < nl).
+template <int MAXL>
+__device__ __forceinline__ double walk_regs(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
+                                            double bL, double aL, double bT, int* nhull,
+                                            const WalkOut* out = nullptr) {
+  int ks = KEY_NONE;
+#pragma unroll
+  for (int t = MAXL - 1; t >= 0; --t) ks = (lane + 64 * t < nl && lb[t] == bL && la[t] == aL) ? lane + 64 * t : ks;
+  ks = wave_min_i32(ks);
+  WalkAcc acc;
+  acc.start(ks, lane, out);
+  double bc = bL, ac = aL;
+  for (int guard = 0; guard < nl; ++guard) {
+    double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
+    int kb = KEY_NONE;
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const int k = lane + 64 * t;
+      if (k < nl && lb[t] > bc) {
+        const double x = (ac - la[t]) / (lb[t] - bc);
+        if (walk_less(x, lb[t], la[t], k, xb, bb, ab, kb)) {
+          xb = x; bb = lb[t]; ab = la[t]; kb = k;
+        }
+      }
+    }
+    if (__ballot(kb != KEY_NONE) == 0) break;
+    const WalkPick p = wave_walk_min(xb, bb, ab, kb);
+    acc.step(p, bc, bT, lane, out);
+    bc = p.b;
+    ac = p.a;
+  }
+  *nhull = acc.h + 1;
+  return acc.finish(lane);
+}
+
+// Exact walk over streamed lines: build(c, la, lb) rebuilds chunk c (line
+// k = c * 64 * MAXL + lane + 64 t) every step.
+template <int MAXL, class Build>
+__device__ __forceinline__ double walk_stream(int nch, int nl, int lane, double bL, double aL, double bT, int* nhull,
+                                              Build&& build, const WalkOut* out = nullptr) {
+  int ks = KEY_NONE;
+  for (int c = nch - 1; c >= 0; --c) {
+    double la[MAXL], lb[MAXL];
+    build(c, la, lb);
+#pragma unroll
+    for (int t = MAXL - 1; t >= 0; --t) {
+      const int k = c * 64 * MAXL + lane + 64 * t;
+      ks = (k < nl && lb[t] == bL && la[t] == aL) ? k : ks;
+    }
+  }
+  ks = wave_min_i32(ks);
+  WalkAcc acc;
+  acc.start(ks, lane, out);
+  double bc = bL, ac = aL;
+  for (int guard = 0; guard < nl; ++guard) {
+    double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
+    int kb = KEY_NONE;
+    for (int c = 0; c < nch; ++c) {
+      double la[MAXL], lb[MAXL];
+      build(c, la, lb);
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) {
+        const int k = c * 64 * MAXL + lane + 64 * t;
+        if (k < nl && lb[t] > bc) {
+          const double x = (ac - la[t]) / (lb[t] - bc);
+          if (walk_less(x, lb[t], la[t], k, xb, bb, ab, kb)) {
+            xb = x; bb = lb[t]; ab = la[t]; kb = k;
+          }
+        }
+      }
+    }
+    if (__ballot(kb != KEY_NONE) == 0) break;
+    const WalkPick p = wave_walk_min(xb, bb, ab, kb);
+    acc.step(p, bc, bT, lane, out);
+    bc = p.b;
+    ac = p.a;
+  }
+  *nhull = acc.h + 1;
+  return acc.finish(lane);
+}
+
+}  // namespace dkg

@@ -7,6 +7,9 @@ in hand-written HIP kernels for gfx950 behind the C ABI of ``include/dkg.h``.
 from .discretekg import (
     DiscreteKnowledgeGradient,
     calculate_discrete_kg,
+    calculate_epigraph_indices,
+    calculate_epigraph_indices_batched,
+    calculate_expected_value_of_piecewise_linear_function,
     calculate_discrete_kg_conditioning_on_single_output,
     kg_from_lines,
     t_batch_mode_transform,
@@ -19,6 +22,9 @@ from .utils import is_power_of_2, make_torch_std_grid, sample_simplex
 __all__ = [
     "DiscreteKnowledgeGradient",
     "calculate_discrete_kg",
+    "calculate_epigraph_indices",
+    "calculate_epigraph_indices_batched",
+    "calculate_expected_value_of_piecewise_linear_function",
     "calculate_discrete_kg_conditioning_on_single_output",
     "kg_from_lines",
     "t_batch_mode_transform",

@@ -15,7 +15,7 @@ from .errors import BotorchTensorDimensionError, DkgNativeError, NotPSDError, Un
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdkg.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 DKG_PLAN_GRAD = 1
 DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
 DKG_PLAN_F32 = 4  # fp32 contractions (BASELINE configs[4]); forward only
@@ -76,6 +76,9 @@ SIGNATURES = {
                                     c_int, POINTER(c_float)]),
     "dkg_plan_hull_sizes": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "dkg_lines_kg": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_epigraph": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dkg_pwl_expectation": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "dkg_plan_lines": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_debug_read_kstamps": (c_int, [c_void_p, c_int]),
     "dkg_debug_wave_ops": (c_int, [c_void_p, c_void_p, c_void_p]),
     "dkg_debug_mfma_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -8,6 +8,8 @@ Same surface as the reference's
   and ``forward(X[*batch, 1, d]) -> [*batch]`` (``:33-159``);
 * ``calculate_discrete_kg`` (``:162-235``) and
   ``calculate_discrete_kg_conditioning_on_single_output`` (``:238-338``);
+* ``calculate_epigraph_indices`` (``:341-412``, the reference's walk exactly) and
+  ``calculate_expected_value_of_piecewise_linear_function`` (``:415-452``), device-backed;
 * ``kg_from_lines`` — the epigraph + expectation stage
   (``calculate_epigraph_indices`` + ``calculate_expected_value_of_piecewise_linear_function``
   + ``- max(intercepts)``, ``:225-233, 341-452``) batched on the device.
@@ -19,6 +21,7 @@ no CPU fallback: without the HIP library or a ROCm device these raise.
 
 from __future__ import annotations
 
+import math
 from functools import wraps
 from typing import Optional
 
@@ -214,6 +217,119 @@ def calculate_discrete_kg_conditioning_on_single_output(model, xnew: Tensor, obj
     return acq(xnew.reshape(1, 1, -1)).reshape(())
 
 
+def _verify_intercepts_and_slopes(intercepts: Tensor, slopes: Tensor) -> None:
+    """The reference's checks and messages (``discretekg.py:455-470``)."""
+    if intercepts.dim() != 1 or slopes.dim() != 1:
+        raise BotorchTensorDimensionError(
+            f"Expected 'intercepts' and 'slopes' to both be one-dimensional tensors. "
+            f"Got {intercepts.dim()=} and {slopes.dim()=}.")
+    if intercepts.shape != slopes.shape:
+        raise BotorchTensorDimensionError(
+            f"Expected 'intercepts' and 'slopes' to have the same shape. "
+            f"Got {intercepts.shape=} and {slopes.shape=}.")
+    if intercepts.shape[-1] == 0:
+        raise ValueError(f"Expected inputs to specify at least one line. Got {intercepts.shape[-1]=}.")
+
+
+def _device_of(t: Tensor) -> torch.device:
+    return t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+
+
+def calculate_epigraph_indices_batched(intercepts: Tensor, slopes: Tensor):
+    """The reference walk (``calculate_epigraph_indices``, ``discretekg.py:341-412``) for a batch
+    of line sets ``[..., L]``, on the device (``dkg_epigraph``).
+
+    Returns ``(indices [..., L] int64, intersections [..., L-1], counts [...] int32)``: set p's
+    envelope is ``indices[p, :counts[p]]`` with breakpoints ``intersections[p, :counts[p]-1]``;
+    entries past the count are -1 / NaN.  Computed in fp64.
+    """
+    if intercepts.shape != slopes.shape:
+        raise BotorchTensorDimensionError(
+            f"Expected 'intercepts' and 'slopes' to have the same shape. "
+            f"Got {intercepts.shape=} and {slopes.shape=}.")
+    if intercepts.dim() < 1:
+        raise BotorchTensorDimensionError("Expected 'intercepts' and 'slopes' to have at least one dimension.")
+    L = intercepts.shape[-1]
+    if L == 0:
+        raise ValueError(f"Expected inputs to specify at least one line. Got intercepts.shape[-1]={L}.")
+    lib = _lib.load()
+    dev = _device_of(intercepts)
+    a = intercepts.detach().to(dev, torch.double).reshape(-1, L).contiguous()
+    b = slopes.detach().to(dev, torch.double).reshape(-1, L).contiguous()
+    P = a.shape[0]
+    idx = torch.full((P, L), -1, dtype=torch.int64, device=dev)
+    xs = torch.full((P, max(L - 1, 1)), float("nan"), dtype=torch.double, device=dev)
+    cnt = torch.zeros(P, dtype=torch.int32, device=dev)
+    _lib.check(lib.dkg_epigraph(_lib.ptr(a), _lib.ptr(b), P, L, L, _lib.ptr(idx), _lib.ptr(xs), _lib.ptr(cnt),
+                                current_stream_ptr(dev)), "dkg_epigraph")
+    shape = intercepts.shape[:-1]
+    return idx.reshape(*shape, L), xs[:, : L - 1].reshape(*shape, L - 1), cnt.reshape(shape)
+
+
+def calculate_epigraph_indices(intercepts: Tensor, slopes: Tensor):
+    """Upper envelope of the lines ``a_k + b_k z`` (``discretekg.py:341-412``), on the device.
+
+    Same results as the reference: the line indices left to right and the intersections
+    between successive ones, the same IEEE values (``include/dkg.h`` ``dkg_epigraph``).  The
+    intersections are recomputed from the returned indices with the reference's expression,
+    so they carry the reference's autograd graph w.r.t. ``intercepts`` / ``slopes``.
+    """
+    _verify_intercepts_and_slopes(intercepts, slopes)
+    idx, xs, cnt = calculate_epigraph_indices_batched(intercepts.reshape(1, -1), slopes.reshape(1, -1))
+    m = int(cnt[0])
+    indices = idx[0, :m].to(intercepts.device)
+    if m < 2:
+        return indices, torch.tensor([], dtype=intercepts.dtype, device=intercepts.device)
+    if intercepts.requires_grad or slopes.requires_grad:
+        i0, i1 = indices[:-1], indices[1:]
+        inter = -(intercepts[i0] - intercepts[i1]) / (slopes[i0] - slopes[i1])  # discretekg.py:394
+    else:
+        inter = xs[0, : m - 1].to(device=intercepts.device, dtype=intercepts.dtype)
+    return indices, inter
+
+
+class _PiecewiseExpectation(torch.autograd.Function):
+    """E[f(Z)] on the device; backward by the closed form of the reference expression
+    (d/da_j = dPhi_j, d/db_j = -dphi_j, d/dc_k = phi(c_k) (a_{k-1} - a_k + c_k (b_{k-1} - b_k)))."""
+
+    @staticmethod
+    def forward(ctx, a, b, c):
+        lib = _lib.load()
+        dev = _device_of(a)
+        m = a.shape[0]
+        ad = a.detach().to(dev, torch.double).contiguous()
+        bd = b.detach().to(dev, torch.double).contiguous()
+        cd = c.detach().to(dev, torch.double).contiguous()
+        out = torch.empty(1, dtype=torch.double, device=dev)
+        _lib.check(lib.dkg_pwl_expectation(_lib.ptr(ad), _lib.ptr(bd), _lib.ptr(cd) if m > 1 else 0, 1, m,
+                                           _lib.ptr(out), current_stream_ptr(dev)), "dkg_pwl_expectation")
+        ctx.save_for_backward(a, b, c)
+        return out.reshape(()).to(device=a.device, dtype=a.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, c = ctx.saved_tensors
+        inf = torch.full((1,), float("inf"), dtype=c.dtype, device=c.device)
+        z = torch.cat([-inf, c, inf])
+        pdf = torch.where(torch.isinf(z), torch.zeros_like(z), torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi))
+        cdf = 0.5 * (1 + torch.erf(z / math.sqrt(2)))
+        ga = (cdf[1:] - cdf[:-1]) * g
+        gb = -(pdf[1:] - pdf[:-1]) * g
+        gc = pdf[1:-1] * ((a[:-1] - a[1:]) + c * (b[:-1] - b[1:])) * g
+        return ga, gb, gc
+
+
+def calculate_expected_value_of_piecewise_linear_function(intercepts: Tensor, slopes: Tensor, boundaries: Tensor):
+    """E[f(Z)] for Z ~ N(0, 1) and piecewise-linear f (``discretekg.py:415-452``), on the device
+    (``dkg_pwl_expectation``, the reference's formula); differentiable."""
+    _verify_intercepts_and_slopes(intercepts, slopes)
+    if boundaries.shape != (len(intercepts) - 1,):
+        raise BotorchTensorDimensionError(
+            f"Expected 'boundaries' to be a one-dimensional tensor with "
+            f"{len(intercepts)} elements. Got {boundaries.shape=}.")
+    return _PiecewiseExpectation.apply(intercepts, slopes, boundaries)
+
+
 def kg_from_lines(intercepts: Tensor, slopes: Tensor, return_hull_size: bool = False):
     """E[max_k (a_k + b_k Z)] - max_k a_k per set of lines, on the device.
 
@@ -230,7 +346,7 @@ def kg_from_lines(intercepts: Tensor, slopes: Tensor, return_hull_size: bool = F
     if L == 0:
         raise ValueError(f"Expected inputs to specify at least one line. Got intercepts.shape[-1]={L}.")
     lib = _lib.load()
-    dev = intercepts.device if intercepts.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    dev = _device_of(intercepts)
     a = intercepts.detach().to(dev, torch.double).reshape(-1, L).contiguous()
     b = slopes.detach().to(dev, torch.double).reshape(-1, L).contiguous()
     P = a.shape[0]

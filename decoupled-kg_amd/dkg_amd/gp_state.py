@@ -194,6 +194,19 @@ class ForwardPlan:
                    "dkg_plan_hull_sizes")
         return kg, pairs, hull
 
+    def lines(self, X: torch.Tensor):
+        """The lines the envelope stage builds for candidates X (B x d), bit for bit:
+        (intercepts, slopes), each [B, S, N + 1] on the device (line 0 = the candidate; dkg_plan_lines)."""
+        X = X.detach().to(self.device, torch.double).contiguous()
+        B = X.shape[0]
+        if B > self.max_B:
+            raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
+        a = torch.empty(B, self.S, self.state.N + 1, dtype=torch.double, device=self.device)
+        b = torch.empty_like(a)
+        _lib.check(_lib.load().dkg_plan_lines(self.host, self._dev_ptr, _lib.ptr(X), B, _lib.ptr(a), _lib.ptr(b),
+                                              current_stream_ptr(self.device)), "dkg_plan_lines")
+        return a, b
+
     def forward_grad(self, X: torch.Tensor):
         """KG[B] and dKG/dx [B, d] for candidates X (B x d): one C call."""
         if not self.grad:

@@ -110,30 +110,96 @@ def from_botorch(model) -> ModelListGPState:
     return ModelListGPState(*outs)
 
 
-def from_state_dict(state: dict, train_x: torch.Tensor, train_y: torch.Tensor,
-                    kernel: str = "matern", nu: float = 2.5) -> ModelListGPState:
-    """ModelListGP ``state_dict`` (raw GPyTorch parameters) + data -> state.
+def _per_output(v, m: int, what: str) -> list:
+    """A shared tensor, or one per output."""
+    if isinstance(v, (list, tuple)):
+        if len(v) != m:
+            raise ValueError(f"{what}: {len(v)} entries for {m} outputs")
+        return [torch.as_tensor(t, dtype=torch.double) for t in v]
+    t = torch.as_tensor(v, dtype=torch.double)
+    if what == "train_y":
+        if t.dim() == 1 and m == 1:
+            return [t]
+        if t.dim() != 2 or t.shape[1] != m:
+            raise ValueError(f"train_y must be n x {m} (or one tensor per output); got shape {tuple(t.shape)}")
+        return [t[:, i] for i in range(m)]
+    return [t] * m
 
-    Raw parameters go through GPyTorch's constraint transform (softplus +
-    lower bound); ``raw_noise = -inf`` therefore maps to the noise lower bound.
+
+def _constrained(sd: dict, key: str, enforced: bool = True) -> torch.Tensor:
+    """A GPyTorch constrained parameter from its raw value: Interval(lb, ub) -> sigmoid, GreaterThan /
+    Positive -> softplus + lb; ``enforced=False`` (a constraint built with ``transform=None``,
+    factory.py:102-104 and BoTorch's default likelihood) -> the raw value itself."""
+    if key not in sd:
+        raise KeyError(f"state dict has no {key!r}")
+    raw = sd[key]
+    if not enforced:
+        return raw
+    lb = sd.get(key + "_constraint.lower_bound", torch.tensor(0.0, dtype=torch.double))
+    ub = sd.get(key + "_constraint.upper_bound", torch.tensor(float("inf"), dtype=torch.double))
+    if bool(torch.isfinite(ub).all()):
+        return lb + (ub - lb) * torch.sigmoid(raw)
+    return torch.nn.functional.softplus(raw) + lb
+
+
+def from_state_dict(state: dict, train_x, train_y, kernel: str = "matern", nu: float = 2.5, bounds=None,
+                    noise_constraint: str = "enforced") -> ModelListGPState:
+    """ModelListGP ``state_dict`` (raw GPyTorch parameters and buffers) + training data -> state.
+
+    * ``train_x``: [n, d] shared by every output, or one [n_i, d] tensor per output (decoupled BO
+      keeps a training set per objective).  With ``bounds`` [2, d] the raw inputs are normalised
+      as the reference does before building each GP (``factory.py:64``), else they must already be
+      in [0, 1]^d.
+    * ``train_y``: [n, m], or one [n_i] tensor per output, in the problem's units (what the reference
+      hands to ``SingleTaskGP``).  If the state dict holds a ``Standardize(m=1)`` outcome transform
+      (``models.i.outcome_transform.means`` / ``stdvs``, ``factory.py:75-76``) the targets are
+      standardised with those buffers exactly as BoTorch did at construction, and the posterior is
+      untransformed with them (``y_mean`` / ``y_std``).
+    * Raw parameters go through GPyTorch's constraint transforms (softplus + lower bound, or sigmoid
+      for a finite interval).  ``noise_constraint="raw"`` for likelihoods whose ``GreaterThan`` was
+      built with ``transform=None`` (the BO loop's models, ``factory.py:102-104``): the noise is the
+      raw value.  The GP-problem fixtures (``data/shared/gp-problem``) enforce it (``raw_noise = -inf``
+      maps to the lower bound).
+    * The constant mean is ``mean_module.raw_constant`` (GPyTorch >= 1.9) or ``mean_module.constant``;
+      a missing mean raises ``KeyError``.
     """
+    if noise_constraint not in ("enforced", "raw"):
+        raise ValueError(f"noise_constraint must be 'enforced' or 'raw', got {noise_constraint!r}")
     sd = {k: torch.as_tensor(v, dtype=torch.double) for k, v in state.items()}
+    m = 0
+    while f"models.{m}.covar_module.raw_outputscale" in sd:
+        m += 1
+    if m == 0:
+        raise KeyError("state dict has no 'models.0.covar_module.raw_outputscale': not a ModelListGP state dict")
+    xs = _per_output(train_x, m, "train_x")
+    ys = _per_output(train_y, m, "train_y")
     outs = []
-    i = 0
-    sp = torch.nn.functional.softplus
-    while f"models.{i}.covar_module.raw_outputscale" in sd:
+    for i in range(m):
         p = f"models.{i}."
-
-        def cons(key):
-            lb = sd.get(p + key + "_constraint.lower_bound", torch.tensor(0.0, dtype=torch.double))
-            return sp(sd[p + key]) + lb
-
+        x = xs[i]
+        if bounds is not None:
+            bnd = torch.as_tensor(bounds, dtype=torch.double)
+            x = (x - bnd[0]) / (bnd[1] - bnd[0])
+        if p + "mean_module.raw_constant" in sd:
+            c = float(sd[p + "mean_module.raw_constant"].reshape(-1)[0])
+        elif p + "mean_module.constant" in sd:
+            c = float(sd[p + "mean_module.constant"].reshape(-1)[0])
+        else:
+            raise KeyError(f"state dict has no constant mean for output {i} "
+                           f"({p}mean_module.raw_constant / {p}mean_module.constant)")
+        y = ys[i].reshape(-1)
+        y_mean, y_std = 0.0, 1.0
+        if p + "outcome_transform.means" in sd:
+            if p + "outcome_transform.stdvs" not in sd:
+                raise KeyError(f"{p}outcome_transform.means without {p}outcome_transform.stdvs")
+            y_mean = float(sd[p + "outcome_transform.means"].reshape(-1)[0])
+            y_std = float(sd[p + "outcome_transform.stdvs"].reshape(-1)[0])
+            y = (y - y_mean) / y_std                      # Standardize.forward (BoTorch)
         outs.append(SingleTaskGPState(
-            train_x=train_x, train_y=train_y[:, i],
-            lengthscale=cons("covar_module.base_kernel.raw_lengthscale").reshape(-1),
-            outputscale=float(cons("covar_module.raw_outputscale")),
-            noise=float(cons("likelihood.noise_covar.raw_noise").reshape(-1)[0]),
-            mean_constant=float(sd.get(p + "mean_module.raw_constant", torch.tensor(0.0))),
-            kernel=kernel, nu=nu))
-        i += 1
+            train_x=x, train_y=y,
+            lengthscale=_constrained(sd, p + "covar_module.base_kernel.raw_lengthscale").reshape(-1),
+            outputscale=float(_constrained(sd, p + "covar_module.raw_outputscale")),
+            noise=float(_constrained(sd, p + "likelihood.noise_covar.raw_noise",
+                                     noise_constraint == "enforced").reshape(-1)[0]),
+            mean_constant=c, kernel=kernel, nu=nu, y_mean=y_mean, y_std=y_std))
     return ModelListGPState(*outs)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 2
+#define DKG_ABI_VERSION 3
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -212,9 +212,39 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
  * and optionally the number of upper-envelope lines n_hull[p] (nullable).
  * Replaces calculate_epigraph_indices + calculate_expected_value_of_piecewise_
  * linear_function + the baseline subtraction (discretekg.py:225-233, 341-452);
- * L = 0 -> DKG_ERR_NO_LINES (the reference's ValueError, :466-470). */
+ * L = 0 -> DKG_ERR_NO_LINES (the reference's ValueError, :466-470).  Any L. */
 int dkg_lines_kg(const double* intercepts, const double* slopes, int P, int L, double* kg, int* n_hull,
                  void* stream);
+
+/* The reference's epigraph, exactly: calculate_epigraph_indices
+ * (discretekg.py:341-412) for P sets of L lines (device, [P][L]).
+ *   indices      : device int64 [P][cap], the envelope's line indices left to right
+ *   intersections: device [P][cap - 1], the breakpoints between them (nullable if cap == 1)
+ *   count        : device int [P], the envelope size m (entries beyond cap are not written)
+ * Same walk as the reference: lines ordered by slope ascending then intercept
+ * descending, each step to the later line of a different slope whose
+ * intersection -(a_i - a_j)/(b_i - b_j) is first, ties to the first in that
+ * order; the intersections are the same IEEE values.  Every |b| < 1e-9 -> the
+ * first line of maximal intercept, no intersections (:363-367).  Among exact
+ * duplicate lines (equal slope and intercept) the lowest index is returned
+ * (the reference's first sort is not stable for more than 16 lines on CPU
+ * torch; any duplicate is an equal line).  L = 0 -> DKG_ERR_NO_LINES. */
+int dkg_epigraph(const double* intercepts, const double* slopes, int P, int L, int cap, long long* indices,
+                 double* intersections, int* count, void* stream);
+
+/* calculate_expected_value_of_piecewise_linear_function (discretekg.py:415-452)
+ * for P functions of m pieces: out[p] = sum_j a_j (Phi(c_j) - Phi(c_{j-1}))
+ * - b_j (phi(c_j) - phi(c_{j-1})), c_0 = -inf, c_m = +inf, boundaries [P][m-1]
+ * (device; nullable when m == 1).  m = 0 -> DKG_ERR_NO_LINES. */
+int dkg_pwl_expectation(const double* intercepts, const double* slopes, const double* boundaries, int P, int m,
+                        double* out, void* stream);
+
+/* The lines the plan's envelope stage builds for candidates xnew (device,
+ * B x d): intercepts / slopes device [B][S][N + 1], line 0 the candidate
+ * itself (discretekg.py:182-223 full, :300-321 decoupled), bit-identical to
+ * the envelope's.  Runs the cross and covariance stages; fp64 plans only. */
+int dkg_plan_lines(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* intercepts,
+                   double* slopes, void* stream);
 
 /* Debug: per-workgroup phase stamps of the three forward kernels, written when
  * the env var DKG_DEBUG_STAMPS=1 at plan creation: [3][1024][8] words (slot 0

@@ -4,9 +4,9 @@ SURVEY.md §8(e): the (candidate x scalarisation) pairs are split across ranks
 and combined with one collective (all-reduce over scalarisations, or
 all-gather over candidates).  Each rank's local evaluation is the oracle
 (injected), so this checks the partitioning and the exchange, not the kernels.
-Tolerance: the suite's KG tolerance (tests/helpers.py: 1e-6 relative plus the
-fp64 cancellation floor) — the oracle's batched matmuls round differently for
-a candidate slice than for the whole batch, at the 1e-14 absolute level.
+Tolerance: the stated one (tests/helpers.py: 1e-6 |KG| + 64 eps max|a|) — the
+oracle's batched matmuls round differently for a candidate slice than for the
+whole batch.
 """
 
 import os
@@ -19,8 +19,8 @@ import torch
 
 from dkg_amd.dist import shard_range
 from dkg_amd.synthetic import WORKLOADS, make_problem
-from helpers import assert_kg_close, rounding_floor, to_oracle
-from oracle.discretekg import discrete_kg_batched
+from helpers import assert_within, stated_tol, to_oracle
+from oracle.discretekg import discrete_kg_batched, lines_batched
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -62,7 +62,8 @@ def test_sharded_matches_unsharded(tmp_path, axis, B, S, target):
     model, D, X, W = make_problem(WORKLOADS["small"])
     om = to_oracle(model)
     ref = discrete_kg_batched(om, X[:B], D, W[:S], target)[0]
-    assert_kg_close(res["kg"], ref, rounding_floor(om, X[:B], D, W[:S], target))
+    amax = lines_batched(om, X[:B], D, W[:S], target)[0].abs().amax((-1, -2))
+    assert_within(res["kg"], ref, stated_tol(ref, amax))
     calls = res["calls"]
     if axis == "scalarisations":
         assert sum(c[0][1] for c in calls if c) == S and all(c[0][0] == B for c in calls if c)

@@ -1,8 +1,12 @@
 """HIP path vs the CPU oracle on identical inputs (needs a real MI355X).
 
 Every check goes through the C ABI (``include/dkg.h``) via ``dkg_amd``.
-Tolerance: |KG_gpu - KG_oracle| <= 1e-6 |KG_oracle| + floor, the floor being
-the fp64 rounding bound of ``helpers.rounding_floor``.
+Tolerance (BASELINE.md "Accuracy"): |KG_gpu - KG_oracle| <= 1e-6 |KG_oracle|
++ 64 eps max|a|.  End to end the lines themselves come out of two fp64 builds of an ill-conditioned
+posterior, so there the bound adds the measured line gap propagated by KG's Lipschitz constants
+(helpers.kg_line_floor: 2 max|da| + sqrt(2/pi) max|db|), and the line gap itself must stay within
+helpers.LINE_RTOL; the envelope kernel alone is held to the stated tolerance on identical lines
+(helpers.parity_case).  Worst ratios: profiles/r02_parity.json (tools/parity_report.py).
 """
 
 import math
@@ -10,7 +14,8 @@ import math
 import pytest
 import torch
 
-from helpers import assert_kg_close, rounding_floor, to_oracle, to_state
+from helpers import (EPS, assert_within, check_parity_case, kg_line_floor, line_gap, parity_case,
+                     stated_tol, to_oracle, to_state)
 from oracle.discretekg import (
     _kg_from_lines,
     calculate_discrete_kg,
@@ -98,8 +103,7 @@ def test_lines_kg_random_sets(L):
     b[12:14] = 1e-10 * b[12:14]       # |b| < 1e-9 everywhere
     got = kg_from_lines(a.to(DEV), b.to(DEV)).cpu()
     ref = _oracle_lines_kg(a, b)
-    floor = 64 * torch.finfo(torch.double).eps * a.abs().amax(-1)
-    assert_kg_close(got, ref, floor)
+    assert_within(got, ref, stated_tol(ref, a.abs().amax(-1)))
     assert bool((got >= 0).all())
 
 
@@ -114,7 +118,7 @@ def test_lines_kg_parabola_many_hull_lines():
     a, b = a[perm][None], b[perm][None]
     got, hull = kg_from_lines(a.to(DEV), b.to(DEV), return_hull_size=True)
     ref = _oracle_lines_kg(a, b)
-    assert_kg_close(got.cpu(), ref, 64 * torch.finfo(torch.double).eps * a.abs().amax(-1))
+    assert_within(got.cpu(), ref, stated_tol(ref, a.abs().amax(-1)))
     assert int(hull) == L
 
 
@@ -162,9 +166,8 @@ def test_reference_kat_table_full(ref_model):
     kg = acq(X)
     torch.testing.assert_close(kg, torch.tensor([[0.0383, 0.0224, 0.0130], [0.0005, 0.0058, 0.0015]]),
                                atol=1e-4, rtol=1e-3)
-    ref = discrete_kg_forward(ref_model, X, reference_test_discretisation(), torch.tensor(TRIO))
-    floor = rounding_floor(ref_model, X.reshape(-1, 2), reference_test_discretisation(), torch.tensor(TRIO))
-    assert_kg_close(kg, ref, floor)
+    check_parity_case(parity_case(to_state(ref_model), reference_test_discretisation(), torch.tensor(TRIO),
+                                  X.reshape(-1, 2), None))
 
 
 def test_reference_kat_table_single_output(ref_model):
@@ -197,6 +200,8 @@ def test_reference_kat_scalars(ref_model):
 @pytest.mark.parametrize("workload", ["small", "parity6d"])
 @pytest.mark.parametrize("target", [None, 0, 1])
 def test_forward_vs_faithful_oracle(workload, target):
+    """The per-candidate, dense-covariance oracle (the reference's structure); tolerance: stated +
+    the line-gap floor measured against the batched oracle's lines (same math, other summation order)."""
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
@@ -206,12 +211,30 @@ def test_forward_vs_faithful_oracle(workload, target):
     got = acq(X.unsqueeze(-2))
     om = to_oracle(model)
     ref = discrete_kg_forward(om, X.unsqueeze(-2), D, W, target)
-    assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
+    a_dev, b_dev = acq._plan_for(16).lines(X.to(DEV))
+    a_ref, b_ref = lines_batched(om, X, D, W, target)
+    da, db = line_gap(a_dev, b_dev, a_ref, b_ref)
+    assert_within(got, ref, stated_tol(ref, a_ref.abs().amax((-1, -2))) + kg_line_floor(da, db))
     assert bool((got >= 0).all())
 
 
+@pytest.mark.parametrize("workload,nX", [("small", 32), ("parity6d", 32), ("headline", 128)])
 @pytest.mark.parametrize("target", [None, 0, 1])
-def test_headline_vs_batched_oracle(target):
+def test_forward_vs_oracle_all_candidates(workload, nX, target):
+    """Every candidate of the workload: lines within LINE_RTOL of the oracle's, the envelope at the
+    stated tolerance on identical lines, and KG end to end (helpers.parity_case)."""
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS[workload])
+    res = parity_case(model, D, W, X[:nX], target)
+    print(f"{workload} target={target}: " + ", ".join(f"{k}={v:.3g}" for k, v in res.items()
+                                                     if not k.startswith("_") and isinstance(v, float)))
+    check_parity_case(res)
+
+
+@pytest.mark.parametrize("target", [None, 0, 1])
+def test_headline_pairs_and_mean(target):
+    """KG per (candidate, scalarisation) of the headline batch; the forward's KG is their mean."""
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
@@ -219,11 +242,6 @@ def test_headline_vs_batched_oracle(target):
     acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)
     pairs = acq.forward_pairs(X.unsqueeze(-2)).cpu()
     got = acq(X.unsqueeze(-2)).cpu()
-    om = to_oracle(model)
-    ref, ref_pairs = discrete_kg_batched(om, X[:48], D, W, target)
-    floor = rounding_floor(om, X[:48], D, W, target)
-    assert_kg_close(got[:48], ref, floor)
-    assert_kg_close(pairs[:48], ref_pairs, floor[:, None].expand_as(ref_pairs))
     torch.testing.assert_close(got, pairs.mean(-1), rtol=1e-14, atol=1e-300)
 
 
@@ -262,11 +280,9 @@ def test_odd_sizes_and_padding():
     W = torch.rand(5, 3, generator=g, dtype=torch.double)
     W = W / W.sum(-1, keepdim=True)
     Xc = torch.rand(19, 3, generator=g, dtype=torch.double)
-    om = to_oracle(model)
     for target in (None, 0, 2):
-        got = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)(Xc.unsqueeze(-2))
-        ref = discrete_kg_forward(om, Xc.unsqueeze(-2), D, W, target)
-        assert_kg_close(got, ref, rounding_floor(om, Xc, D, W, target))
+        check_parity_case(parity_case(model, D, W, Xc, target))
+        DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)(Xc.unsqueeze(-2))
 
 
 def test_matern12_single_output_and_no_weights():
@@ -280,9 +296,9 @@ def test_matern12_single_output_and_no_weights():
     D = torch.rand(100, 2, generator=g, dtype=torch.double)
     Xc = torch.rand(10, 1, 2, generator=g, dtype=torch.double)
     got = DiscreteKnowledgeGradient(model, D)(Xc)
-    om = to_oracle(model)
-    ref = discrete_kg_forward(om, Xc, D, torch.tensor([[1.0]]))
-    assert_kg_close(got, ref, rounding_floor(om, Xc.squeeze(1), D, torch.tensor([[1.0]])))
+    res = parity_case(model, D, torch.tensor([[1.0]], dtype=torch.double), Xc.squeeze(1), None)
+    check_parity_case(res)
+    torch.testing.assert_close(got.cpu(), res["_tensors"][0], rtol=0, atol=0)
 
 
 def test_lines_match_oracle_lines_headline():
@@ -296,7 +312,7 @@ def test_lines_match_oracle_lines_headline():
     got = kg_from_lines(a.to(DEV), b.to(DEV)).cpu()
     ref = torch.stack([torch.stack([_kg_from_lines(a[i, j], b[i, j]) for j in range(a.shape[1])])
                        for i in range(a.shape[0])])
-    assert_kg_close(got, ref, 64 * torch.finfo(torch.double).eps * a.abs().amax(-1))
+    assert_within(got, ref, stated_tol(ref, a.abs().amax(-1)))
     del DiscreteKnowledgeGradient
 
 
@@ -325,35 +341,21 @@ def test_wave_butterfly_primitives():
 def test_stress_config_parity(target):
     """BASELINE.json configs[4] shape (m=3, n=1024, N=4096 = 64^2 grid, S=32), fp64:
     the envelope streams its 4097 lines per pair from global memory."""
-    from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
     model, D, X, W = make_problem(WORKLOADS["stress"])
-    X = X[:4]
-    om = to_oracle(model)
-    ref, _ = discrete_kg_batched(om, X, D, W, target)
-    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
-    assert acq._plan_for(4).state is not None
-    got = acq(X.to(DEV).unsqueeze(-2)).cpu()
-    assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
+    check_parity_case(parity_case(model, D, W, X[:4], target))
 
 
 @pytest.mark.parametrize("target", [None, 1])
 def test_stress_refinement_parity(target):
-    """Streaming envelope at the stress shape over 24 candidates x 32 scalarisations: ~16 % of the pairs
-    have more chord survivors than the hull stage takes (SURVEY-shaped data, max ~900 of 4097 lines) and go
-    through the quickhull refinement of the survivor list (refine_list) instead of the gift wrap."""
-    from dkg_amd import DiscreteKnowledgeGradient
+    """Streaming envelope at the stress shape over 24 candidates x 32 scalarisations: long candidate
+    lists (the stress lines keep up to ~2000 of 4097 lines near the chords L-T / T-R) go through the
+    streamed quickhull rounds before the walk."""
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
     model, D, X, W = make_problem(WORKLOADS["stress32"])
-    X = X[:24]
-    om = to_oracle(model)
-    ref, _ = discrete_kg_batched(om, X, D, W, target)
-    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
-    pairs = acq.forward_pairs(X.to(DEV).unsqueeze(-2)).cpu()
-    got = pairs.mean(-1)
-    assert_kg_close(got, ref, rounding_floor(om, X, D, W, target))
+    check_parity_case(parity_case(model, D, W, X[:24], target))
 
 
 # ---------------------------------------------------------------- fp32 contractions (DKG_PLAN_F32)
@@ -411,27 +413,8 @@ def test_f32_refuses_gradient():
 
 
 # ---------------------------------------------------------------- envelope sizes (dkg_plan_hull_sizes)
-@pytest.mark.parametrize("workload,nX", [("small", 8), ("parity6d", 8), ("stress32", 4)])
-def test_envelope_sizes_match_reference_walk(workload, nX):
-    """The number of upper-envelope lines per (candidate, scalarisation) that the envelope stage reports
-    (register hull, quickhull-refined lists and the streamed walk alike) equals len(indices) of the
-    reference walk (calculate_epigraph_indices, discretekg.py:341-412) on the oracle's lines."""
-    from dkg_amd import DiscreteKnowledgeGradient
-    from dkg_amd.synthetic import WORKLOADS, make_problem
-    from oracle.discretekg import calculate_epigraph_indices, lines_batched
-
-    model, D, X, W = make_problem(WORKLOADS[workload])
-    X = X[:nX]
-    a, b = lines_batched(to_oracle(model), X, D, W, None)
-    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
-    kg, pairs, hull = acq._plan_for(nX).forward_stats(X.to(DEV))
-    ref = torch.tensor([[len(calculate_epigraph_indices(a[i, j], b[i, j])[0]) for j in range(W.shape[0])]
-                        for i in range(nX)])
-    got = hull.cpu().long()
-    agree = float((got == ref).double().mean())
-    # near-collinear vertices may be classified differently under the two roundings of the lines
-    assert agree >= 0.95 and int((got - ref).abs().max()) <= 2, f"agree {agree:.3f}, ref {ref.tolist()}, got {got.tolist()}"
-    torch.testing.assert_close(pairs.mean(-1), kg, rtol=1e-12, atol=1e-300)
+# The forward's envelope sizes equal the reference walk's on the same lines exactly:
+# tests/test_gpu_epigraph.py::test_forward_envelopes_are_the_reference_walk.
 
 
 def test_concurrent_plans_on_streams_match_single_stream():
