@@ -17,7 +17,7 @@ namespace dkg {
 // boundaries, 7 = s_memrealtime at end.  `dst` is a kernel argument, so
 // production launches pay no dependent load for it.
 __device__ __forceinline__ unsigned long long* kst_slot(int dst, const Plan* P, int kid) {
-  if (!dst) return nullptr;
+  if (dst != 1) return nullptr;
   const int wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   return (threadIdx.x == 0 && wg < KST_WG) ? P->kstamps + ((size_t)kid * KST_WG + wg) * 8 : nullptr;
 }
@@ -287,16 +287,21 @@ __device__ __forceinline__ int first_max_index(const double (&la)[MAXL], int nl,
 
 // KG_w (and the envelope size) of register-held lines: build(la, lb) fills the
 // lines (line k in lane k % 64, slot k / 64; k >= nl: NaN intercepts); it runs
-// again only for the overflow walk, so no register line is live across the
-// list walk.  force_walk: test hook (every set takes the walk over all lines).
+// again only for a second filter or the walk over all lines, so no register
+// line is live across the list walk.  force_walk: test hook (every set takes
+// the walk over all lines).  pst (debug, DKG_DEBUG_STAMPS=2): phase stamps.
 template <int MAXL, class Build>
 __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
-                                                bool force_walk, int* nhull, const WalkOut* out = nullptr) {
+                                                bool force_walk, int* nhull, const WalkOut* out = nullptr,
+                                                unsigned long long* pst = nullptr) {
   FwdEnv f;
+  if (pst) pst[0] = __builtin_amdgcn_s_memtime();
   {
     double la[MAXL], lb[MAXL];
     build(la, lb);
+    if (pst) pst[1] = __builtin_amdgcn_s_memtime();
     f = env_extremes<MAXL>(la, lb);
+    if (pst) pst[2] = __builtin_amdgcn_s_memtime();
     if (f.status == 1) {
       if (out && out->cap > 0) {
         const int k = first_max_index<MAXL>(la, nl, lane, f.aT);
@@ -306,23 +311,47 @@ __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane,
       return 0.0;
     }
     f.cnt = env_compact<MAXL, ENV_CAP>(la, lb, env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR), lane, sb, sa, si);
+    if (pst) {
+      pst[3] = __builtin_amdgcn_s_memtime();
+      pst[6] = (unsigned long long)f.cnt;
+    }
   }
-  if (f.cnt <= ENV_CAP && !force_walk) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double cmax;
-    int h;
-    const double kg = (f.cnt <= 64) ? walk_list<1>(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out)
-                                    : walk_list<2>(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
-    if (uniform(cmax <= WALK_XGUARD)) {
-      *nhull = h;
-      return kg;
+  if (!force_walk) {
+    double rel = WALK_MARGIN;
+    for (int level = 0; level < 2; ++level) {
+      if (f.cnt > ENV_CAP) break;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double cmax;
+      int h;
+      const double kg = walk_small(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
+      if (pst) pst[4] = __builtin_amdgcn_s_memtime();
+      if (uniform(cmax <= rel * WALK_POW2_50)) {
+        *nhull = h;
+        if (pst) pst[7] = (unsigned long long)h | ((unsigned long long)level << 33);
+        return kg;
+      }
+      // a breakpoint beyond the guard: filter again with the margin that covers it
+      rel = WALK_REFILTER * cmax / WALK_POW2_50;
+      if (!uniform(rel < WALK_REL_MAX) || level == 1) break;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double la[MAXL], lb[MAXL];
+      build(la, lb);
+      f.cnt = env_compact<MAXL, ENV_CAP>(la, lb, env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR, rel), lane, sb, sa,
+                                         si);
     }
   }
   double la[MAXL], lb[MAXL];
   build(la, lb);
-  return walk_regs<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bT, nhull, out);
+  const double kgw = walk_regs<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bT, nhull, out);
+  if (pst) {
+    pst[5] = __builtin_amdgcn_s_memtime();
+    pst[7] = (unsigned long long)(*nhull) | (1ull << 32);
+  }
+  return kgw;
 }
 
 // ---------------------------------------------------------------------------
@@ -859,8 +888,7 @@ __device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, dou
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double cmax, kg;
     int h;
-    if (cnt <= 64) kg = walk_list<1>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
-    else if (cnt <= 128) kg = walk_list<2>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
+    if (cnt <= 128) kg = walk_small(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
     else if (cnt <= 256) kg = walk_list<4>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
     else kg = walk_list<8>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
     if (uniform(cmax <= WALK_XGUARD)) {
@@ -1526,7 +1554,9 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       // the lines are rebuilt from the staged LDS data if the list walk cannot finish,
       // so no register line is live across it
       auto rebuild = [&](double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
-      kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn);
+      unsigned long long* pst = (dst == 2 && lane == 0 && (size_t)b * S + j < 2 * KST_WG)
+                                    ? P->kstamps + ((size_t)b * S + j) * 8 : nullptr;
+      kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst);
     }
     if (pairs_out != nullptr && lane == 0) {
       pairs_out[(size_t)b * S + j] = kgj;

@@ -35,6 +35,15 @@ constexpr int KEY_NONE = 0x7fffffff;
 // the list walk is provably the full walk: 2^20 < 2^23 / 6.
 constexpr double WALK_MARGIN = 9.313225746154785e-10;  // 2^-30
 constexpr double WALK_XGUARD = 1048576.0;              // 2^20
+// The guard for a relative margin rel is rel * 2^50 (the same derivation:
+// rel (1 - 3u) / (6u) > rel * 2^50 with u = 2^-53).  A list walk whose largest
+// breakpoint leaves the first guard is redone over a list filtered with the
+// margin WALK_REFILTER * (that breakpoint) * 2^-50, whose guard is then
+// WALK_REFILTER times the breakpoint; the walk over all lines runs only when
+// that margin would reach WALK_REL_MAX (the filter would keep most lines).
+constexpr double WALK_POW2_50 = 1125899906842624.0;    // 2^50
+constexpr double WALK_REFILTER = 16.0;
+constexpr double WALK_REL_MAX = 0.00390625;            // 2^-8
 
 // psi(c) = E[(Z - c)_+] with the far tail cut to its fp64 value (0 beyond
 // c = 40: exp(-800) underflows), so an infinite breakpoint gives 0, not NaN.
@@ -137,15 +146,16 @@ struct EnvChords {
   double db1, da1, k1, db2, da2, k2;
 };
 
-__device__ __forceinline__ EnvChords env_chords(double bL, double aL, double bT, double aT, double bR, double aR) {
+__device__ __forceinline__ EnvChords env_chords(double bL, double aL, double bT, double aT, double bR, double aR,
+                                                double rel = WALK_MARGIN) {
   EnvChords c;
   const double Wb = bR - bL;
   c.db1 = bT - bL;
   c.da1 = aT - aL;
   c.db2 = bR - bT;
   c.da2 = aR - aT;
-  const double t1 = WALK_MARGIN * (fmax(fabs(aL), fabs(aT)) * c.db1 + fmax(fabs(bL), fabs(bT)) * fabs(c.da1) + Wb * c.db1);
-  const double t2 = WALK_MARGIN * (fmax(fabs(aT), fabs(aR)) * c.db2 + fmax(fabs(bT), fabs(bR)) * fabs(c.da2) + Wb * c.db2);
+  const double t1 = rel * (fmax(fabs(aL), fabs(aT)) * c.db1 + fmax(fabs(bL), fabs(bT)) * fabs(c.da1) + Wb * c.db1);
+  const double t2 = rel * (fmax(fabs(aT), fabs(aR)) * c.db2 + fmax(fabs(bT), fabs(bR)) * fabs(c.da2) + Wb * c.db2);
   c.k1 = (c.db1 > 0.0) ? fma(aL, c.db1, -(bL * c.da1)) - t1 : INFINITY;
   c.k2 = (c.db2 > 0.0) ? fma(aT, c.db2, -(bT * c.da2)) - t2 : INFINITY;
   return c;
@@ -202,6 +212,92 @@ __device__ __forceinline__ double walk_list(int nc, int lane, const double* sb, 
   *nhull = acc.h + 1;
   *cmax = acc.cmax;
   return acc.finish(lane);
+}
+
+// Exact walk over a short candidate list (nc <= R <= 32 entries) by a
+// successor table: row i (lanes G i .. G i + G - 1, G = 64 / R) evaluates the
+// walk step from entry i over its share j = g + G q (q < R / G) of the list,
+// keeps the lane's best under the walk key, and a DPP minimum over the row's
+// lanes gives the row's best intersection.  Every entry's successor is so
+// known at once; the walk is then a chase of row winners by scalar mask
+// operations and one v_readlane per step (the reference's sequence of argmin
+// steps, :382-401, each step's argmin being exactly the row's).  A row whose
+// minimum is attained by several lanes (concurrent lines, duplicates) is
+// resolved by the full key over those lanes (wave_walk_min).  The KG edge
+// terms are evaluated by the winning lanes in parallel.  Returns KG_w;
+// *cmax = 0 when every breakpoint is within WALK_XGUARD, else the largest
+// |breakpoint|.
+template <int R>
+__device__ __forceinline__ double walk_table(int nc, int lane, const double* sb, const double* sa, const int* si,
+                                             double bL, double aL, double bT, int* nhull, double* cmax,
+                                             const WalkOut* out = nullptr) {
+  constexpr int G = 64 / R, JL = R / G;
+  const int i = lane / G, g = lane % G;
+  const int ii = min(i, nc - 1);
+  const double bi = sb[ii], ai = sa[ii];
+  double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
+  int kb = KEY_NONE, jb = -1;
+#pragma unroll
+  for (int q = 0; q < JL; ++q) {
+    const int j = g + G * q;
+    const int jj = min(j, nc - 1);
+    const double bj = sb[jj], aj = sa[jj];
+    const int kj = si[jj];
+    const double x = (ai - aj) / (bj - bi);
+    if (j < nc && bj > bi && walk_less(x, bj, aj, kj, xb, bb, ab, kb)) {
+      xb = x; bb = bj; ab = aj; kb = kj; jb = j;
+    }
+  }
+  double xm = xb;
+  if constexpr (G >= 2) xm = fmin_raw(xm, dpp_f64<0xB1>(xm));
+  if constexpr (G >= 4) xm = fmin_raw(xm, dpp_f64<0x4E>(xm));
+  if constexpr (G >= 8) xm = fmin_raw(xm, dpp_f64<0x141>(xm));
+  const uint64_t hits = __ballot(i < nc && jb >= 0 && xb == xm);
+  // start: the first list position holding L (the list is in line-index order)
+  const uint64_t lead = __ballot(g == 0 && i < nc && bi == bL && ai == aL);
+  int cur = (int)__builtin_ctzll(lead) / G;
+  if (out && lane == 0 && out->cap > 0) out->idx[0] = si[cur];
+  uint64_t win = 0;
+  int h = 0;
+  constexpr uint64_t ROW = (G == 64) ? ~0ull : ((1ull << G) - 1);
+  for (int guard = 0; guard < nc; ++guard) {
+    const uint64_t rm = hits & (ROW << (cur * G));
+    if (rm == 0) break;
+    int w = (int)__builtin_ctzll(rm);
+    if (__popcll(rm) > 1) {  // several lanes at the row minimum: the full key decides
+      const bool sel = (rm >> lane) & 1;
+      const WalkPick p = wave_walk_min(sel ? xb : INFINITY, sel ? bb : INFINITY, sel ? ab : -INFINITY,
+                                       sel ? kb : KEY_NONE);
+      w = (int)__builtin_ctzll(__ballot(sel && kb == p.k));
+    }
+    win |= 1ull << w;
+    if (out && h + 1 < out->cap) {
+      const int kw = __builtin_amdgcn_readlane(kb, w);
+      const double xw = readlane_f64(xb, w);
+      if (lane == 0) {
+        out->idx[h + 1] = kw;
+        out->x[h] = xw;
+      }
+    }
+    cur = __builtin_amdgcn_readlane(jb, w);
+    ++h;
+  }
+  const bool won = (win >> lane) & 1;
+  *nhull = h + 1;
+  *cmax = (__ballot(won && !(fabs(xb) <= WALK_XGUARD)) != 0) ? wave_max(won ? fabs(xb) : 0.0) : 0.0;
+  return wave_sum(won ? (bb - bi) * psi_edge((bb <= bT) ? -xb : xb) : 0.0);
+}
+
+// Walk over the candidate list: the successor table up to 32 entries, the
+// step-by-step argmin walk beyond (PL list entries per lane).
+__device__ __forceinline__ double walk_small(int nc, int lane, const double* sb, const double* sa, const int* si,
+                                             double bL, double aL, double bT, int* nhull, double* cmax,
+                                             const WalkOut* out = nullptr) {
+  if (nc <= 8) return walk_table<8>(nc, lane, sb, sa, si, bL, aL, bT, nhull, cmax, out);
+  if (nc <= 16) return walk_table<16>(nc, lane, sb, sa, si, bL, aL, bT, nhull, cmax, out);
+  if (nc <= 32) return walk_table<32>(nc, lane, sb, sa, si, bL, aL, bT, nhull, cmax, out);
+  if (nc <= 64) return walk_list<1>(nc, lane, sb, sa, si, bL, aL, bT, nhull, cmax, out);
+  return walk_list<2>(nc, lane, sb, sa, si, bL, aL, bT, nhull, cmax, out);
 }
 
 // Exact walk over all register lines (line k = lane + 64 t, k < nl).

@@ -1,0 +1,71 @@
+"""Per-pair phase stamps of the forward envelope (DKG_DEBUG_STAMPS=2).
+
+Run on the GPU box from the repo root:  python tools/pair_stamps.py [workload]
+For every (candidate, scalarisation) pair of the last of 10 forwards: s_memtime
+cycles of the line build, the extremes, the margin chord compaction and the
+list walk, the list length and the envelope size (whether the walk over all
+lines was needed).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "decoupled-kg_amd")]
+os.environ["DKG_DEBUG_STAMPS"] = "2"
+import torch  # noqa: E402
+
+from dkg_amd import DiscreteKnowledgeGradient, _lib  # noqa: E402
+from dkg_amd.synthetic import WORKLOADS, make_problem  # noqa: E402
+
+w = WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "headline"]
+target = int(sys.argv[2]) if len(sys.argv) > 2 else None
+model, D, X, W = make_problem(w)
+acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target)
+plan = acq._plan_for(w.B)
+Xd = X.cuda().contiguous()
+kg = torch.empty(w.B, dtype=torch.double, device="cuda")
+n = 3 * 1024 * 8
+lib = _lib.load()
+for _ in range(10):
+    plan.forward_into(Xd, kg)
+torch.cuda.synchronize()
+buf = (ctypes.c_ulonglong * n)()
+_lib.check(lib.dkg_debug_read_kstamps(buf, n), "kstamps")
+st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+P = min(w.B * w.S, st.shape[0])
+st = st[:P]
+ok = st[:, 3] > st[:, 0]
+s = st[ok]
+build = s[:, 1] - s[:, 0]
+ext = s[:, 2] - s[:, 1]
+comp = s[:, 3] - s[:, 2]
+walked = s[:, 4] > s[:, 3]
+walk = np.where(walked, s[:, 4] - s[:, 3], 0)
+full = (s[:, 7] >> 32) & 1
+refilt = (s[:, 7] >> 33) & 1
+hull = s[:, 7] & 0xffffffff
+cnt = s[:, 6]
+
+
+def q(v):
+    v = np.asarray(v)
+    if v.size == 0:
+        return "-"
+    return f"median {np.median(v):8.0f}  mean {v.mean():8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}"
+
+
+print(f"pairs {P}, with stamps {ok.sum()} (the rest short-circuited)")
+print("build   ", q(build))
+print("extremes", q(ext))
+print("compact ", q(comp))
+print("walk    ", q(walk[walked]))
+print("list cnt", q(cnt))
+print("hull    ", q(hull), " full-walk pairs", int(full.sum()), " refiltered pairs", int(refilt.sum()))
+print("list cnt hist", np.bincount(np.minimum(cnt, 130)).nonzero()[0][:40].tolist())
+for lo, hi in [(0, 8), (8, 16), (16, 32), (32, 64), (64, 129), (129, 10**9)]:
+    sel = (cnt >= lo) & (cnt < hi)
+    if sel.any():
+        print(f"  cnt [{lo},{hi}): {sel.sum():5d} pairs, walk {q(walk[sel & walked])}")
