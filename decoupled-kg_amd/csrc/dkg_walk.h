@@ -31,10 +31,10 @@
 namespace dkg {
 
 constexpr int KEY_NONE = 0x7fffffff;
-// Relative chord margin 2^-30 (EnvChords) and the breakpoint bound under which
-// the list walk is provably the full walk: 2^20 < 2^23 / 6.
-constexpr double WALK_MARGIN = 9.313225746154785e-10;  // 2^-30
-constexpr double WALK_XGUARD = 1048576.0;              // 2^20
+// Relative chord margin 2^-20 (EnvChords) and the breakpoint bound under which
+// the list walk is provably the full walk: 2^30 < 2^33 / 6.
+constexpr double WALK_MARGIN = 9.5367431640625e-07;    // 2^-20
+constexpr double WALK_XGUARD = 1073741824.0;           // 2^30
 // The guard for a relative margin rel is rel * 2^50 (the same derivation:
 // rel (1 - 3u) / (6u) > rel * 2^50 with u = 2^-53).  A list walk whose largest
 // breakpoint leaves the first guard is redone over a list filtered with the
@@ -136,33 +136,33 @@ struct WalkAcc {
 };
 
 // Chords L-T and T-R of the candidate filter with the margin: a line (a, b)
-// is kept iff fma(a, db, -(b da)) >= k for either chord, where
-// k = fma(a0, db, -(b0 da)) - tau, tau = 2^-30 (max|a_end| db + max|b_end| |da| + (b_R - b_L) db):
-// the margin is at least 2^-30 (b_R - b_L) in intercept units at the line's
-// slope.  Exact copies of the chord ends evaluate to k + tau, so L, T, R and
-// their duplicates are always kept.  A degenerate chord (db = 0, then da = 0)
-// keeps nothing.
+// is kept iff fma(-s, b, a) >= K for either chord, s = da / db its slope in
+// the (b, a) plane and K = fma(-s, b0, a0) - tau with
+// tau = rel (max|a_end| + |s| (max|b_end| + Wb) + Wb), Wb = b_R - b_L: the
+// margin is at least rel Wb in intercept units, and the rounding of the test
+// itself (a few ulps of |a| + |s b|, and of s db against da) is far inside it.
+// Exact copies of the chord ends evaluate to at least K, so L, T, R and their
+// duplicates are always kept.  A degenerate chord (db = 0) keeps nothing.
 struct EnvChords {
-  double db1, da1, k1, db2, da2, k2;
+  double s1, k1, s2, k2;
 };
 
 __device__ __forceinline__ EnvChords env_chords(double bL, double aL, double bT, double aT, double bR, double aR,
                                                 double rel = WALK_MARGIN) {
   EnvChords c;
   const double Wb = bR - bL;
-  c.db1 = bT - bL;
-  c.da1 = aT - aL;
-  c.db2 = bR - bT;
-  c.da2 = aR - aT;
-  const double t1 = rel * (fmax(fabs(aL), fabs(aT)) * c.db1 + fmax(fabs(bL), fabs(bT)) * fabs(c.da1) + Wb * c.db1);
-  const double t2 = rel * (fmax(fabs(aT), fabs(aR)) * c.db2 + fmax(fabs(bT), fabs(bR)) * fabs(c.da2) + Wb * c.db2);
-  c.k1 = (c.db1 > 0.0) ? fma(aL, c.db1, -(bL * c.da1)) - t1 : INFINITY;
-  c.k2 = (c.db2 > 0.0) ? fma(aT, c.db2, -(bT * c.da2)) - t2 : INFINITY;
+  const double db1 = bT - bL, db2 = bR - bT;
+  c.s1 = (db1 > 0.0) ? (aT - aL) / db1 : 0.0;
+  c.s2 = (db2 > 0.0) ? (aR - aT) / db2 : 0.0;
+  const double t1 = rel * (fmax(fabs(aL), fabs(aT)) + fabs(c.s1) * (fmax(fabs(bL), fabs(bT)) + Wb) + Wb);
+  const double t2 = rel * (fmax(fabs(aT), fabs(aR)) + fabs(c.s2) * (fmax(fabs(bT), fabs(bR)) + Wb) + Wb);
+  c.k1 = (db1 > 0.0) ? fma(-c.s1, bL, aL) - t1 : INFINITY;
+  c.k2 = (db2 > 0.0) ? fma(-c.s2, bT, aT) - t2 : INFINITY;
   return c;
 }
 
 __device__ __forceinline__ bool env_keep(const EnvChords& c, double a, double b) {
-  return fma(a, c.db1, -(b * c.da1)) >= c.k1 || fma(a, c.db2, -(b * c.da2)) >= c.k2;
+  return fma(-c.s1, b, a) >= c.k1 || fma(-c.s2, b, a) >= c.k2;
 }
 
 // Exact walk over the candidate list (sb, sa, si; nc <= 64 PL entries) from
@@ -235,14 +235,22 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
   const int i = lane / G, g = lane % G;
   const int ii = min(i, nc - 1);
   const double bi = sb[ii], ai = sa[ii];
+  double ebj[JL], eaj[JL];
+  int ekj[JL];
+#pragma unroll
+  for (int q = 0; q < JL; ++q) {  // every entry of the lane's share first: one LDS round trip
+    const int jj = min(g + G * q, nc - 1);
+    ebj[q] = sb[jj];
+    eaj[q] = sa[jj];
+    ekj[q] = si[jj];
+  }
   double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
   int kb = KEY_NONE, jb = -1;
 #pragma unroll
   for (int q = 0; q < JL; ++q) {
     const int j = g + G * q;
-    const int jj = min(j, nc - 1);
-    const double bj = sb[jj], aj = sa[jj];
-    const int kj = si[jj];
+    const double bj = ebj[q], aj = eaj[q];
+    const int kj = ekj[q];
     const double x = (ai - aj) / (bj - bi);
     if (j < nc && bj > bi && walk_less(x, bj, aj, kj, xb, bb, ab, kb)) {
       xb = x; bb = bj; ab = aj; kb = kj; jb = j;
@@ -285,7 +293,10 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
   const bool won = (win >> lane) & 1;
   *nhull = h + 1;
   *cmax = (__ballot(won && !(fabs(xb) <= WALK_XGUARD)) != 0) ? wave_max(won ? fabs(xb) : 0.0) : 0.0;
-  return wave_sum(won ? (bb - bi) * psi_edge((bb <= bT) ? -xb : xb) : 0.0);
+  const double ec = (bb <= bT) ? -xb : xb;
+  // every edge beyond psi_edge's cut: KG_w = 0 exactly (skip exp / erfc)
+  if (__ballot(won && ec <= 40.0) == 0) return 0.0;
+  return wave_sum(won ? (bb - bi) * psi_edge(ec) : 0.0);
 }
 
 // Walk over the candidate list: the successor table up to 32 entries, the
