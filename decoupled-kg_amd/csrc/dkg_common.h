@@ -249,6 +249,10 @@ __device__ __forceinline__ double wave_max(double v) {
   return combine_rows(v, [](double a, double b) { return fmax(a, b); });
 }
 
+// Wave ballot of a compare: the compare's lane mask itself (HIP's __ballot
+// goes through an int and costs a v_cndmask + v_cmp per use).
+__device__ __forceinline__ uint64_t ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
 // A condition every lane agrees on, made visibly wave-uniform (scalar branch,
 // full EXEC) so cross-lane operations inside the branch see every lane.
 __device__ __forceinline__ bool uniform(bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; }

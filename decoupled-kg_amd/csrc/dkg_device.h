@@ -166,7 +166,7 @@ __device__ __forceinline__ EnvFilter envelope_filter(const double (&la)[MAXL], c
     // the list carries their indices (lowest index among duplicates) and the
     // max-a count without another pass over the lines
     if constexpr (IDX) s = s || a == aT || (bb == bL && a == aL) || (bb == bR && a == aR);
-    const uint64_t mk = __ballot(s);
+    const uint64_t mk = ballot(s);
     if (mk != 0) {  // wave-uniform, rarely taken
       if (s) {
         const int pos = cnt + lanes_below(mk);
@@ -254,22 +254,24 @@ __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const d
 template <int MAXL, int CAP>
 __device__ __forceinline__ int env_compact(const double (&la)[MAXL], const double (&lb)[MAXL], const EnvChords& ch,
                                            int lane, double* sb, double* sa, int* si) {
+  // every slot's keep mask first (independent compares, no branch between
+  // them), then the writes of the slots that keep anything (few)
+  uint64_t mk[MAXL];
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) mk[t] = env_keep_mask(ch, la[t], lb[t]);
   int cnt = 0;
 #pragma unroll
   for (int t = 0; t < MAXL; ++t) {
-    const double a = la[t], bb = lb[t];
-    const bool s = env_keep(ch, a, bb);
-    const uint64_t mk = __ballot(s);
-    if (mk != 0) {  // wave-uniform, rarely taken
-      if (s) {
-        const int pos = cnt + lanes_below(mk);
+    if (mk[t] != 0) {  // wave-uniform, rarely taken
+      if ((mk[t] >> lane) & 1) {
+        const int pos = cnt + lanes_below(mk[t]);
         if (pos < CAP) {
-          sb[pos] = bb;
-          sa[pos] = a;
+          sb[pos] = lb[t];
+          sa[pos] = la[t];
           si[pos] = lane + 64 * t;
         }
       }
-      cnt += __popcll(mk);
+      cnt += __popcll(mk[t]);
     }
   }
   return cnt;
@@ -397,12 +399,12 @@ __device__ __forceinline__ HullGrad envelope_hull_grad(const EnvFilter& f, int l
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     if (ok[c] && lb_[c] == f.bL && la_[c] == f.aL) kst = min(kst, li_[c]);
-    cntT += __popcll(__ballot(ok[c] && la_[c] == f.aT));
+    cntT += __popcll(ballot(ok[c] && la_[c] == f.aT));
   }
   kst = wave_min_i32(kst);
   int start;
   {
-    const uint64_t m0 = __ballot(ok[0] && li_[0] == kst), m1 = __ballot(ok[1] && li_[1] == kst);
+    const uint64_t m0 = ballot(ok[0] && li_[0] == kst), m1 = ballot(ok[1] && li_[1] == kst);
     start = m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1);
   }
   // right neighbour of every entry (as envelope_hull)
@@ -465,7 +467,7 @@ __device__ __forceinline__ HullGrad envelope_hull_grad(const EnvFilter& f, int l
       if (li_[c] == 0) { pw0 = Pw; dw0 = Dw; }
     }
     const bool q = on[c] && li_[c] >= 1 && li_[c] <= N;
-    const uint64_t mq = __ballot(q);
+    const uint64_t mq = ballot(q);
     if (q) {
       const int pos = nq + lanes_below(mq);
       hk[pos] = li_[c];
@@ -544,7 +546,7 @@ __device__ __forceinline__ EnvFilter envelope_filter_stream(int nch, int lane, d
       const double a = la[t], bb = lb[t];
       bool s = fma(a, db1, -bb * da1) > k1 || fma(a, db2, -bb * da2) > k2;
       if constexpr (IDX) s = s || a == aT || (bb == bL && a == aL) || (bb == bR && a == aR);
-      const uint64_t mk = __ballot(s);
+      const uint64_t mk = ballot(s);
       if (mk != 0) {
         if (s) {
           const int pos = cnt + lanes_below(mk);
@@ -768,7 +770,7 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
       const int k = ch * 64 * MAXL + lane + 64 * t;
       const int c = chord_of<MAXL, NV2, Build>(lb[t], wb_, nv);
       const bool keep = k < nl && chord_keep_reg<NV2>(lb[t], la[t], wb_, wa_, c, Wb);
-      const uint64_t mk = __ballot(keep);
+      const uint64_t mk = ballot(keep);
       if (mk != 0) {
         if (keep) {
           const int pos = cnt + lanes_below(mk);
@@ -867,7 +869,7 @@ __device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, dou
     for (int t = 0; t < MAXL; ++t) {
       const int k = c * 64 * MAXL + lane + 64 * t;
       const bool s = k < nl && env_keep(ch, la[t], lb[t]);
-      const uint64_t mk = __ballot(s);
+      const uint64_t mk = ballot(s);
       if (mk != 0) {
         if (s) {
           const int pos = cnt + lanes_below(mk);
@@ -1484,7 +1486,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
             kL = (lb[t] == f.bL && la[t] == f.aL) ? k : kL;
             kT = (la[t] == f.aT && lb[t] == f.bT) ? k : kT;
             kR = (lb[t] == f.bR && la[t] == f.aR) ? k : kR;
-            ct += __popcll(__ballot(la[t] == f.aT));
+            ct += __popcll(ballot(la[t] == f.aT));
           }
         };
         if constexpr (STREAM) {

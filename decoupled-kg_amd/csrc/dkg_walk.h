@@ -68,7 +68,7 @@ __device__ __forceinline__ WalkPick wave_walk_min(double x, double b, double a, 
   double xm = x;
   DKG_BUTTERFLY_ROW({ xm = fmin_raw(xm, partner_f64<S_>(xm)); })
   xm = combine_rows(xm, [](double p, double q) { return fmin(p, q); });
-  const uint64_t tie = __ballot(x == xm);
+  const uint64_t tie = ballot(x == xm);
   WalkPick r;
   r.x = xm;
   if (__popcll(tie) == 1) {
@@ -165,6 +165,11 @@ __device__ __forceinline__ bool env_keep(const EnvChords& c, double a, double b)
   return fma(-c.s1, b, a) >= c.k1 || fma(-c.s2, b, a) >= c.k2;
 }
 
+// The wave's keep mask: the two compares' lane masks OR-ed (no VGPR round trip).
+__device__ __forceinline__ uint64_t env_keep_mask(const EnvChords& c, double a, double b) {
+  return ballot(fma(-c.s1, b, a) >= c.k1) | ballot(fma(-c.s2, b, a) >= c.k2);
+}
+
 // Exact walk over the candidate list (sb, sa, si; nc <= 64 PL entries) from
 // the lowest-index copy of L = (bL, aL).  Returns KG_w (cancellation-free edge
 // sum); *nhull = envelope lines; *cmax = largest |breakpoint| (the caller
@@ -203,7 +208,7 @@ __device__ __forceinline__ double walk_list(int nc, int lane, const double* sb, 
         }
       }
     }
-    if (__ballot(kb != KEY_NONE) == 0) break;
+    if (ballot(kb != KEY_NONE) == 0) break;
     const WalkPick p = wave_walk_min(xb, bb, ab, kb);
     acc.step(p, bc, bT, lane, out);
     bc = p.b;
@@ -260,9 +265,9 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
   if constexpr (G >= 2) xm = fmin_raw(xm, dpp_f64<0xB1>(xm));
   if constexpr (G >= 4) xm = fmin_raw(xm, dpp_f64<0x4E>(xm));
   if constexpr (G >= 8) xm = fmin_raw(xm, dpp_f64<0x141>(xm));
-  const uint64_t hits = __ballot(i < nc && jb >= 0 && xb == xm);
+  const uint64_t hits = ballot(i < nc && jb >= 0 && xb == xm);
   // start: the first list position holding L (the list is in line-index order)
-  const uint64_t lead = __ballot(g == 0 && i < nc && bi == bL && ai == aL);
+  const uint64_t lead = ballot(g == 0 && i < nc && bi == bL && ai == aL);
   int cur = (int)__builtin_ctzll(lead) / G;
   if (out && lane == 0 && out->cap > 0) out->idx[0] = si[cur];
   uint64_t win = 0;
@@ -276,7 +281,7 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
       const bool sel = (rm >> lane) & 1;
       const WalkPick p = wave_walk_min(sel ? xb : INFINITY, sel ? bb : INFINITY, sel ? ab : -INFINITY,
                                        sel ? kb : KEY_NONE);
-      w = (int)__builtin_ctzll(__ballot(sel && kb == p.k));
+      w = (int)__builtin_ctzll(ballot(sel && kb == p.k));
     }
     win |= 1ull << w;
     if (out && h + 1 < out->cap) {
@@ -292,10 +297,10 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
   }
   const bool won = (win >> lane) & 1;
   *nhull = h + 1;
-  *cmax = (__ballot(won && !(fabs(xb) <= WALK_XGUARD)) != 0) ? wave_max(won ? fabs(xb) : 0.0) : 0.0;
+  *cmax = (ballot(won && !(fabs(xb) <= WALK_XGUARD)) != 0) ? wave_max(won ? fabs(xb) : 0.0) : 0.0;
   const double ec = (bb <= bT) ? -xb : xb;
   // every edge beyond psi_edge's cut: KG_w = 0 exactly (skip exp / erfc)
-  if (__ballot(won && ec <= 40.0) == 0) return 0.0;
+  if (ballot(won && ec <= 40.0) == 0) return 0.0;
   return wave_sum(won ? (bb - bi) * psi_edge(ec) : 0.0);
 }
 
@@ -336,7 +341,7 @@ __device__ __forceinline__ double walk_regs(const double (&la)[MAXL], const doub
         }
       }
     }
-    if (__ballot(kb != KEY_NONE) == 0) break;
+    if (ballot(kb != KEY_NONE) == 0) break;
     const WalkPick p = wave_walk_min(xb, bb, ab, kb);
     acc.step(p, bc, bT, lane, out);
     bc = p.b;
@@ -382,7 +387,7 @@ __device__ __forceinline__ double walk_stream(int nch, int nl, int lane, double 
         }
       }
     }
-    if (__ballot(kb != KEY_NONE) == 0) break;
+    if (ballot(kb != KEY_NONE) == 0) break;
     const WalkPick p = wave_walk_min(xb, bb, ab, kb);
     acc.step(p, bc, bT, lane, out);
     bc = p.b;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # envelope: margin 2^-20, slope-form chord test, preloaded table, psi skip
 set -uo pipefail
-out=gpurun_out/r02g
+out=gpurun_out/r02h
 mkdir -p "$out"
 timeout -k 10 500 python3 -u -m pytest tests/test_gpu_epigraph.py tests/test_gpu_parity.py tests/test_gpu_grad.py -x -q --timeout 200 --timeout-method thread -m gpu > "$out/tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 "$out/tests.log"; [ $rc -eq 0 ] || exit $rc
