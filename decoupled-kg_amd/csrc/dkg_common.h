@@ -152,10 +152,12 @@ __host__ __device__ inline int dim_bucket(int d) { return d <= 2 ? 2 : d <= 4 ? 
 // row_half_mirror; row_mirror), then two cross-row exchanges.  Each step
 // hands every lane the value of a partner lane in the other half of its
 // current group; with a commutative combine all lanes end with the same result.
+// (mov_dpp: every lane is written by these full-row patterns, so no "old"
+// value, and no v_mov to set one up, is needed.)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
 
@@ -230,10 +232,10 @@ __device__ __forceinline__ double combine_rows(double v, Op op) {
 
 // Wave minimum of an int: the four in-row DPP steps, then the four row values by v_readlane.
 __device__ __forceinline__ int wave_min_i32(int v) {
-  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false));
   const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
   const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
   return min(min(r0, r1), min(r2, r3));

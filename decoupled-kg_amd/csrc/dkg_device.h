@@ -254,24 +254,28 @@ __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const d
 template <int MAXL, int CAP>
 __device__ __forceinline__ int env_compact(const double (&la)[MAXL], const double (&lb)[MAXL], const EnvChords& ch,
                                            int lane, double* sb, double* sa, int* si) {
-  // every slot's keep mask first (independent compares, no branch between
-  // them), then the writes of the slots that keep anything (few)
-  uint64_t mk[MAXL];
-#pragma unroll
-  for (int t = 0; t < MAXL; ++t) mk[t] = env_keep_mask(ch, la[t], lb[t]);
+  // the keep masks of a group of four slots first (independent compares, no
+  // branch between them), then the group's writes (rarely any)
   int cnt = 0;
 #pragma unroll
-  for (int t = 0; t < MAXL; ++t) {
-    if (mk[t] != 0) {  // wave-uniform, rarely taken
-      if ((mk[t] >> lane) & 1) {
-        const int pos = cnt + lanes_below(mk[t]);
-        if (pos < CAP) {
-          sb[pos] = lb[t];
-          sa[pos] = la[t];
-          si[pos] = lane + 64 * t;
+  for (int t0 = 0; t0 < MAXL; t0 += 4) {
+    uint64_t mk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) mk[u] = (t0 + u < MAXL) ? env_keep_mask(ch, la[t0 + u], lb[t0 + u]) : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u;
+      if (t < MAXL && mk[u] != 0) {  // wave-uniform, rarely taken
+        if ((mk[u] >> lane) & 1) {
+          const int pos = cnt + lanes_below(mk[u]);
+          if (pos < CAP) {
+            sb[pos] = lb[t];
+            sa[pos] = la[t];
+            si[pos] = lane + 64 * t;
+          }
         }
+        cnt += __popcll(mk[u]);
       }
-      cnt += __popcll(mk[t]);
     }
   }
   return cnt;

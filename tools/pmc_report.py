@@ -1,0 +1,76 @@
+"""Aggregate tools/pmc_passes.sh output into per-kernel, per-launch figures.
+
+usage: python tools/pmc_report.py <outdir> <profiles/tag.json>
+
+Per kernel (forward instantiations only): average per launch of every counter,
+per-wave instruction mix, VALU / MFMA busy fractions and HBM bytes.  Units and
+gfx950 corrections (MI355X_MICROARCH.md "HBM", "Per-instruction cycle constants"):
+  * FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE reports half the bytes of a
+    16-B-per-lane streaming read -> x2 for the read side (an estimate for 8-B loads);
+  * SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_* count quad-cycles (x4);
+  * SQ_BUSY_CYCLES counts cycles per SE-sampled SQ (reported raw);
+  * SQ_VALU_MFMA_BUSY_CYCLES counts cycles, summed over the SIMDs.
+"""
+import csv
+import glob
+import json
+import sys
+
+KERNELS = {"cross_root_plan_kernel": "cross_root_kernel", "posterior_cov_kernel": "posterior_cov_kernel",
+           "envelope_kernel": "envelope_kernel"}
+CLOCK_GHZ = 2.4
+SIMDS = 1024
+
+
+def load(out):
+    agg = {}
+    for f in glob.glob(f"{out}/*/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            kn = r["Kernel_Name"]
+            for k, name in KERNELS.items():
+                if k in kn and not (k == "envelope_kernel" and ", true," in kn):
+                    agg.setdefault(name, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {n: {c: sum(v) / len(v) for c, v in d.items()} for n, d in agg.items()}
+
+
+def durations(out):
+    d = {}
+    for f in glob.glob(f"{out}/trace/**/*kernel_stats.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            for k, name in KERNELS.items():
+                if k in r["Name"] and not (k == "envelope_kernel" and ", true," in r["Name"]):
+                    d[name] = float(r["AverageNs"]) / 1e3
+    return d
+
+
+def main():
+    out, dst = sys.argv[1], sys.argv[2]
+    avg, dur = load(out), durations(out)
+    rep = {}
+    for name, c in avg.items():
+        w = c.get("SQ_WAVES", 0.0) or 1.0
+        r = {"counters_per_launch": c, "avg_us": dur.get(name)}
+        r["per_wave"] = {k[3:]: v / w for k, v in c.items() if k.startswith("SQ_INSTS") or k in (
+            "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
+            "SQ_ACTIVE_INST_LDS")}
+        if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+            r["hbm_bytes_per_launch"] = (2.0 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024.0
+            r["fetch_bytes_x2"] = 2.0 * c.get("FETCH_SIZE", 0.0) * 1024.0
+            r["write_bytes"] = c.get("WRITE_SIZE", 0.0) * 1024.0
+        if dur.get(name):
+            simd_cycles = dur[name] * 1e-6 * CLOCK_GHZ * 1e9 * SIMDS
+            if "SQ_ACTIVE_INST_VALU" in c:
+                r["valu_busy_frac"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / simd_cycles
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+                r["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+            if "SQ_INSTS_VALU_MFMA_MOPS_F64" in c:
+                # MOPS counts 512-flop units per the gfx94x convention (16x16x4 f64 = 2 MOPS)
+                r["mfma_f64_tflops_from_mops"] = c["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512 / (dur[name] * 1e-6) / 1e12
+        rep[name] = r
+    json.dump(rep, open(dst, "w"), indent=2)
+    print(json.dumps({n: {k: v for k, v in r.items() if k != "counters_per_launch"} for n, r in rep.items()},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
