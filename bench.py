@@ -4,21 +4,30 @@ One step = one DiscreteKnowledgeGradient forward over a batch of B candidates
 per GPU (the reference's ``forward(X[B,1,d])``, discretekg.py:131-159) at the
 headline workload: m=2 outputs, n_train=256, n_disc=1024 (32x32 std grid),
 S=16 scalarisations, B=128 candidates per GPU, d=2, fp64.  Inputs and GP state
-are resident in HBM before timing.  For N>1 (torchrun, one rank per GPU,
-RCCL) each rank evaluates its own 128 candidates (weak scaling) and the
-per-candidate KG values of every ``--exchange-every`` steps are all-gathered in
-one async RCCL call (double buffered), so every rank ends with the whole batch
-of every step.  ``--shard scalarisations`` instead gives every rank the same 128
-candidates and its own 16 weight rows (16*N in total) and combines the
-per-candidate partial sums with one async RCCL all-reduce per exchange (the
-north-star exchange; SURVEY.md §8(e) amortises it over K forward batches,
-count = K*B, because one collective costs about as much host and link latency as
-a whole 128-candidate forward); ``value`` then counts headline-equivalent evals
-(candidates x 16 scalarisations).
+are resident in HBM before timing.
 
-Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus the
-roofline of the dominant kernel (HIP-event timed, same stream) and a bounded
-CPU baseline of the oracle restatement on the host cores.
+For N>1 (torchrun, one rank per GPU, RCCL) the default ``--shard
+scalarisations`` is the north-star layout (BASELINE.json north_star, SURVEY.md
+§8(e)): every rank evaluates the same 128 candidates on its own 16 weight rows
+(16*N rows in total, weak scaling) and the per-candidate partial sums meet in
+one async RCCL all-reduce per ``--exchange-every`` forward batches (count =
+K*B; SURVEY §8(e) amortises the collective over K batches because one small
+collective costs about as much host and link latency as a whole forward);
+``value`` counts headline-equivalent evals (candidates x 16 scalarisations).
+``--shard candidates`` gives every rank its own 128 candidates on all 16 rows and
+all-gathers the per-candidate values instead.
+
+Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus
+  * ``roofline``: the dominant kernel's duration (HIP events on its launch
+    stream) against the ceiling that binds it: the envelope is
+    VALU-issue bound (it does comparisons and selects, not counted flops), so its
+    fraction is VALU-busy SIMD cycles (PMC count per launch, profiles/) over the
+    SIMD cycles of the live launch; every stage is listed in ``stages``;
+  * ``cpu_baseline``: a bounded sample of the oracle restatement on the host cores;
+  * ``nondegenerate``: the same throughput path on headline sizes with KG > 0 for
+    every pair (d = 6; the envelope does real work);
+  * ``latency_b1``: value+gradient at B = 1, the ``optimize_acqf`` call shape of the
+    reference's production loop (bo_loop.py:127-129, batch_limit=1).
 """
 
 import argparse
@@ -36,9 +45,16 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
-FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix
+# MI355X peaks.  Spec (MI355X_MICROARCH.md / SURVEY 8(d)): 78.6 TF fp64 (vector = matrix), 157.3 TF fp32
+# matrix, 8 TB/s HBM.  Measured on the box (tools/ubench/rates.hip, profiles/r02a_rates_f64.txt):
+# v_mfma_f64_16x16x4 77.2 TF, v_fma_f64 61.4 TF.
+FP64_PEAK_TFLOPS = 78.6
+FP64_MFMA_MEASURED_TFLOPS = 77.2
+FP64_VALU_MEASURED_TFLOPS = 61.4
+FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
+SIMDS, CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMDs
+PMC_REPORT = os.path.join(REPO, "profiles", "r02", "pmc_headline.json")
 
 
 def parse():
@@ -47,7 +63,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=1024)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", default="headline")
-    ap.add_argument("--shard", choices=["candidates", "scalarisations"], default="candidates",
+    ap.add_argument("--shard", choices=["scalarisations", "candidates"], default="scalarisations",
                     help="axis of the (candidate x scalarisation) space split over ranks (weak scaling)")
     ap.add_argument("--exchange-every", type=int, default=256,
                     help="forward batches per RCCL exchange (count = K*B fp64 values)")
@@ -55,20 +71,24 @@ def parse():
     ap.add_argument("--precision", choices=["fp64", "fp32"], default="fp64",
                     help="fp32: the contractions in fp32 MFMA (DKG_PLAN_F32; BASELINE configs[4], workload stress32)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: the process's CPU affinity (os.sched_getaffinity), capped by OMP_NUM_THREADS if set")
     ap.add_argument("--profile-reps", type=int, default=50)
     ap.add_argument("--streams", type=int, default=4,
                     help="forward batches in flight: step k runs on stream k %% streams with its own plan workspace")
     ap.add_argument("--graph", type=int, default=1,
                     help="1 = replay each full exchange period (E forwards over the streams) as one captured HIP graph")
-    ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls (0 = skip)")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_headline.json"),
-                    help="per-kernel HBM traffic from a rocprofv3 --pmc pass (tools/pmc_summary.py)")
+    ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")
+    ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
+    ap.add_argument("--nd-steps", type=int, default=256,
+                    help="timed steps of the non-degenerate headline-size leg (workload headline_nd; 0 = skip)")
+    ap.add_argument("--pmc", default=PMC_REPORT,
+                    help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py)")
     return ap.parse_args()
 
 
 def stage_model(w, m, n, N, B, S, d):
-    """Algorithmic flops / HBM bytes per launch of each kernel (DESIGN.md 'Roofline')."""
+    """Algorithmic flops / HBM bytes per launch of each kernel."""
     kev = 3 * d + 8  # flops per kernel evaluation (distance + Matern profile)
     fl_cross = sum(B * nn * (nn + 1) + 2 * B * nn + B * nn * kev for nn in n)
     fl_cov = sum(2 * B * N * nn + B * N * kev for nn in n)
@@ -89,11 +109,29 @@ def survey_model(m, n, N, S, B, d):
     return f_eval * B, by
 
 
-def cpu_baseline(model, D, W, X, target, seconds, threads):
+def cpu_info(requested: int):
+    aff = len(os.sched_getaffinity(0))
+    threads = requested or aff
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if not requested and omp and omp.isdigit():
+        threads = min(threads, int(omp))   # the GPU box's CPU share (OMP_NUM_THREADS=16 there)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, aff, model
+
+
+def cpu_baseline(model, D, W, X, target, seconds, threads_req):
     """The oracle's structure-faithful restatement of the reference path on host cores."""
     from oracle.discretekg import calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output
     from oracle.gp import ModelList, OutputGP
 
+    threads, aff, cpu_model = cpu_info(threads_req)
     torch.set_num_threads(threads)
     om = ModelList([OutputGP(m.train_x, m.train_y, m.lengthscale, m.outputscale, m.noise, m.mean_constant,
                              m.kernel, m.nu, m.y_mean, m.y_std) for m in model.models])
@@ -112,64 +150,31 @@ def cpu_baseline(model, D, W, X, target, seconds, threads):
         cnt += 1
     dt = time.perf_counter() - t0
     return {"value": cnt / dt, "unit": "KG-evals/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model, "affinity_cpus": aff,
             "sample": f"{cnt} forwards cycling over the {Xc.shape[0]} headline candidates (per-candidate loop, "
-                      f"dense (N+1)^2 posterior covariance, reference epigraph walk; torch fp64 CPU), "
-                      f"{dt:.1f} s"}
+                      f"dense (N+1)^2 posterior covariance, reference epigraph walk; torch fp64 CPU, "
+                      f"{threads} threads), {dt:.1f} s"}
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    # DKG_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with several ranks on one GPU (not a bench line)
-    backend = os.environ.get("DKG_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local %= max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+class Throughput:
+    """The timed throughput path: E forward batches per exchange, ``streams`` batches in flight, one
+    captured HIP graph per exchange buffer (DESIGN.md §6 "Forward batches in flight")."""
 
-    from dkg_amd import DiscreteKnowledgeGradient
-    from dkg_amd.synthetic import WORKLOADS, make_problem
-    from dkg_amd.utils import sample_simplex
+    def __init__(self, acq, X, B, E, mode, S_local, dev, precision):
+        from dkg_amd.dist import BatchExchange
 
-    w = WORKLOADS[args.workload]
-    model, D, X0, W = make_problem(w)
-    X = X0
-    if args.shard == "candidates":
-        # weak scaling: every rank evaluates its own B candidates (Sobol stream per rank)
-        if rank > 0:
-            X = torch.quasirandom.SobolEngine(w.d, scramble=True, seed=4 + 1000 * rank).draw(w.B, dtype=torch.double)
-        W_local = W
-    else:
-        # weak scaling: S rows per rank out of S*world (rank 0's rows are the headline W)
-        W_all = W if world == 1 else torch.cat([W, sample_simplex(w.m, w.S * (world - 1), qmc=True, seed=99)])
-        W_local = W_all[rank * w.S:(rank + 1) * w.S]
-    acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev,
-                                    precision=args.precision)
-    plan = acq._plan_for(w.B)
-    Xd = X.to(dev).contiguous()
-    E = max(1, min(args.exchange_every, args.steps))
-    from dkg_amd.dist import BatchExchange
-    xchg = BatchExchange(w.B, E, "gather" if args.shard == "candidates" else "reduce", S_local=w.S, device=dev)
+        self.acq, self.B, self.E, self.dev = acq, B, E, dev
+        self.plan = acq._plan_for(B)
+        self.Xd = X.to(dev).contiguous()
+        self.xchg = BatchExchange(B, E, mode, S_local=S_local, device=dev)
+        self.main = torch.cuda.current_stream(dev)
+        self.f32 = precision == "fp32"
 
-    main_s = torch.cuda.current_stream(dev)
-
-    def timed(ns, steps, warmup, graph=False):
-        """Warmup + `steps` timed forwards with `ns` forward batches in flight.  Stream i (i = k % ns)
-        runs step k through its own plan (own Q_X / cov workspace); a stream waits on the main stream
-        whenever a new exchange buffer starts, and the main stream waits on every stream before an
-        exchange, so each collective sees completed rows and a row is never rewritten under one."""
+    def run(self, ns, steps, warmup, graph, world):
+        E, xchg, main_s, dev = self.E, self.xchg, self.main, self.dev
         streams = [main_s] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
-        plans = [plan] + [acq._state.plan(acq._W, acq.target_output_ix, plan.max_B, f32=args.precision == "fp32")
-                          for _ in range(ns - 1)]
+        plans = [self.plan] + [self.acq._state.plan(self.acq._W, self.acq._target, self.plan.max_B, f32=self.f32)
+                               for _ in range(ns - 1)]
 
         def join():
             for s in streams[1:]:
@@ -181,7 +186,7 @@ def main():
                 for s in streams[1:]:
                     s.wait_stream(main_s)
             with torch.cuda.stream(streams[k % ns]):
-                plans[k % ns].forward_into(Xd, kg)
+                plans[k % ns].forward_into(self.Xd, kg)
             if k % E == E - 1:
                 join()
             xchg.done(k)
@@ -191,7 +196,6 @@ def main():
         join()
         xchg.flush(warmup)
         torch.cuda.synchronize()
-
         graphs = []
         if graph and steps >= E:
             # one graph per exchange buffer: the E forwards of a period, forked over the streams exactly
@@ -206,7 +210,7 @@ def main():
                         s.wait_stream(cs)
                     for r in range(E):
                         with torch.cuda.stream(lanes[r % ns]):
-                            plans[r % ns].forward_into(Xd, xchg.bufs[slot][r])
+                            plans[r % ns].forward_into(self.Xd, xchg.bufs[slot][r])
                     for s in lanes[1:]:
                         cs.wait_stream(s)
                 graphs.append(g)
@@ -241,33 +245,121 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t)
 
+
+def batch_stats(plan, Xd):
+    """SURVEY.md 8(d) diagnostics of one batch: short-circuit rate, KG distribution, envelope sizes."""
+    kg_s, pairs_s, hull_s = plan.forward_stats(Xd)
+    pairs_c, hull_c, kg_c = pairs_s.cpu(), hull_s.cpu().long(), kg_s.cpu()
+    hist = torch.bincount(hull_c.reshape(-1)).tolist()
+    return {"pairs": int(pairs_c.numel()),
+            "short_circuit_frac": float((hull_c == 1).double().mean()),
+            "zero_kg_frac": float((pairs_c == 0).double().mean()),
+            "envelope_lines_mean": float(hull_c.double().mean()),
+            "envelope_lines_hist": {str(h): c for h, c in enumerate(hist) if c},
+            "kg_quantiles": {str(q): float(torch.quantile(kg_c, q)) for q in (0.0, 0.1, 0.5, 0.9, 1.0)}}
+
+
+def stage_rooflines(plan, Xd, model_fb, reps, precision, pmc):
+    """Every forward kernel against the ceiling that binds it.  Durations: HIP events around `reps`
+    back-to-back launches of the kernel alone on its own stream (dkg_plan_time_stage)."""
+    names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
+    avg_ms = [plan.time_stage(Xd, k, reps) for k in range(3)]
+    out = {}
+    for i, name in enumerate(names):
+        fl, by = model_fb[name]
+        t = avg_ms[i] * 1e-3
+        r = {"avg_launch_us": t * 1e6, "algorithmic_flops": fl, "algorithmic_bytes": by,
+             "hbm_gbs_algorithmic": by / t / 1e9}
+        p = pmc.get(name, {})
+        traffic = p.get("hbm_bytes_per_launch")
+        if name == "posterior_cov_kernel":
+            peak = FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else FP64_PEAK_TFLOPS
+            ach = fl / t / 1e12
+            r.update({"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+                      "frac_of_measured_peak": ach / FP64_MFMA_MEASURED_TFLOPS,
+                      "mfma_busy_frac_pmc": p.get("mfma_busy_frac")})
+        else:
+            # VALU-issue bound: the envelope's comparisons / selects and cross_root's exp / sqrt fill
+            # are not flops; the fraction is VALU-busy SIMD cycles (PMC SQ_ACTIVE_INST_VALU x 4 quad-cycles,
+            # per launch) over the SIMD cycles of this launch
+            busy = p.get("valu_busy_simd_cycles")
+            ach = busy / t if busy else None
+            peak = SIMDS * CLOCK_GHZ * 1e9
+            r.update({"bound": "valu", "achieved": ach, "peak": peak, "unit": "VALU-busy SIMD-cycles/s",
+                      "frac": (ach / peak) if ach else None,
+                      "counted_fp64_tflops": fl / t / 1e12,
+                      "counted_flop_frac_of_valu_peak": fl / t / 1e12 / FP64_VALU_MEASURED_TFLOPS,
+                      "valu_insts_per_wave": p.get("valu_insts_per_wave")})
+        r["traffic"] = traffic
+        out[name] = r
+    return out
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # DKG_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with several ranks on one GPU (not a bench line)
+    backend = os.environ.get("DKG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+    from dkg_amd.utils import sample_simplex
+
+    def setup(wname):
+        w = WORKLOADS[wname]
+        model, D, X0, W = make_problem(w)
+        X = X0
+        if args.shard == "candidates":
+            # weak scaling: every rank evaluates its own B candidates (Sobol stream per rank)
+            if rank > 0:
+                X = torch.quasirandom.SobolEngine(w.d, scramble=True, seed=4 + 1000 * rank).draw(w.B, dtype=torch.double)
+            W_local = W
+        else:
+            # weak scaling: S rows per rank out of S*world (rank 0's rows are the workload's W)
+            W_all = W if world == 1 else torch.cat([W, sample_simplex(w.m, w.S * (world - 1), qmc=True, seed=99)])
+            W_local = W_all[rank * w.S:(rank + 1) * w.S]
+        acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev,
+                                        precision=args.precision)
+        E = max(1, min(args.exchange_every, args.steps))
+        tp = Throughput(acq, X, w.B, E, "gather" if args.shard == "candidates" else "reduce", w.S, dev,
+                        args.precision)
+        return w, model, D, X0, W, acq, tp
+
+    w, model, D, X0, W, acq, tp = setup(args.workload)
     single = None
     if args.streams > 1 or args.graph:
-        e1 = timed(1, args.steps, args.warmup)
+        e1 = tp.run(1, args.steps, args.warmup, False, world)
         single = {"value": world * w.B * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
-    elapsed = timed(max(1, args.streams), args.steps, args.warmup, graph=bool(args.graph))
+    elapsed = tp.run(max(1, args.streams), args.steps, args.warmup, bool(args.graph), world)
     value = world * w.B * args.steps / elapsed
 
-    # ---- per-kernel durations (HIP events on the launch stream), roofline of the dominant kernel
-    names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
-    avg_ms = [plan.time_stage(Xd, k, args.profile_reps) for k in range(3)]
-    model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)
-    dom = max(range(3), key=lambda i: avg_ms[i])
-    fl, by = model_fb[names[dom]]
-    # every stage is fp64-compute bound (DESIGN.md "Roofline"): MFMA for cross/cov, fp64 VALU (same 78.6 TF
-    # peak) for the envelope; HBM bytes per launch are << peak*duration for all three.
-    peak = FP32_MFMA_PEAK_TFLOPS if (args.precision == "fp32" and dom < 2) else FP64_PEAK_TFLOPS
-    bound, ach, unit = "mfma", fl / (avg_ms[dom] * 1e-3) / 1e12, "TFLOP/s"
-    traffic = None
+    # ---- per-kernel rooflines; the dominant kernel's is the line's `roofline`
+    pmc = {}
     if os.path.exists(args.pmc):
         try:
-            traffic = json.load(open(args.pmc)).get(names[dom], {}).get("hbm_bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
-    roof = {"kernel": names[dom], "bound": bound, "achieved": ach, "peak": peak, "unit": unit,
-            "frac": ach / peak, "traffic": traffic, "algorithmic_flops": fl, "algorithmic_bytes": by,
-            "avg_launch_us": avg_ms[dom] * 1e3,
-            "stages_us": {n: a * 1e3 for n, a in zip(names, avg_ms)}}
+            pmc = json.load(open(args.pmc))
+        except (OSError, ValueError):
+            pmc = {}
+    model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)
+    stages = stage_rooflines(tp.plan, tp.Xd, model_fb, args.profile_reps, args.precision, pmc)
+    dom = max(stages, key=lambda k: stages[k]["avg_launch_us"])
+    roof = dict(stages[dom], kernel=dom,
+                stages={k: {kk: v[kk] for kk in ("avg_launch_us", "bound", "frac", "traffic")}
+                        for k, v in stages.items()},
+                pmc_source=os.path.relpath(args.pmc, REPO) if pmc else None)
 
     # ---- whole-forward roofline as BASELINE.md defines it: max(F/P, Bytes/BW) / T_measured
     f_fwd, b_fwd = survey_model(w.m, [mm.num_train for mm in model.models], D.shape[0], w.S, w.B, w.d)
@@ -275,37 +367,59 @@ def main():
     t_min = max(f_fwd / (FP64_PEAK_TFLOPS * 1e12), b_fwd / (HBM_PEAK_GBS * 1e9))
     fwd_roof = {"definition": "BASELINE.md: max(F/P_fp64, Bytes/BW_HBM) / T_forward", "flops": f_fwd,
                 "bytes": b_fwd, "t_min_us": t_min * 1e6, "t_forward_us": t_fwd * 1e6, "frac": t_min / t_fwd}
-
-    # ---- SURVEY.md 8(d) diagnostics of the batch: short-circuit rate, KG distribution, envelope sizes
-    kg_s, pairs_s, hull_s = plan.forward_stats(Xd)
-    pairs_c, hull_c, kg_c = pairs_s.cpu(), hull_s.cpu().long(), kg_s.cpu()
-    hist = torch.bincount(hull_c.reshape(-1)).tolist()
-    pair_stats = {"pairs": int(pairs_c.numel()),
-                  "short_circuit_frac": float((hull_c == 1).double().mean()),
-                  "zero_kg_frac": float((pairs_c == 0).double().mean()),
-                  "envelope_lines_mean": float(hull_c.double().mean()),
-                  "envelope_lines_hist": {str(h): c for h, c in enumerate(hist) if c},
-                  "kg_quantiles": {str(q): float(torch.quantile(kg_c, q)) for q in (0.0, 0.1, 0.5, 0.9, 1.0)}}
+    stats = batch_stats(tp.plan, tp.Xd)
 
     # ---- value + gradient (dkg_plan_forward_grad: the optimize_acqf L-BFGS-B path), same batch
     grad_info = None
-    if args.grad_steps > 0 and args.precision == "fp64":
-        gplan = acq._plan_for(w.B, grad=True)
-        for _ in range(3):
-            gplan.forward_grad(Xd)
-        torch.cuda.synchronize()
-        g0 = time.perf_counter()
-        for _ in range(args.grad_steps):
-            gplan.forward_grad(Xd)
-        torch.cuda.synchronize()
-        gdt = (time.perf_counter() - g0) / args.grad_steps
-        grad_info = {"value": w.B / gdt, "unit": "KG-evals+gradients/s (per GPU)", "ms_per_step": gdt * 1e3}
+    lat_b1 = None
+    if args.precision == "fp64":
+        if args.grad_steps > 0:
+            gplan = acq._plan_for(w.B, grad=True)
+            for _ in range(3):
+                gplan.forward_grad(tp.Xd)
+            torch.cuda.synchronize()
+            g0 = time.perf_counter()
+            for _ in range(args.grad_steps):
+                gplan.forward_grad(tp.Xd)
+            torch.cuda.synchronize()
+            gdt = (time.perf_counter() - g0) / args.grad_steps
+            grad_info = {"value": w.B / gdt, "unit": "KG-evals+gradients/s (per GPU)", "ms_per_step": gdt * 1e3}
+        if args.b1_calls > 0:
+            # B = 1: the reference's production call shape (bo_loop.py:127-129), one synchronous C call
+            # per L-BFGS-B evaluation; the host needs the value and gradient back each time
+            p1 = acq._plan_for(1, grad=True)
+            for _ in range(5):
+                p1.forward_grad(tp.Xd[:1].contiguous())
+            torch.cuda.synchronize()
+            ts = []
+            for i in range(args.b1_calls):
+                x1 = tp.Xd[i % w.B:i % w.B + 1].contiguous()
+                t0 = time.perf_counter()
+                kg1, g1 = p1.forward_grad(x1)
+                kg1.cpu(), g1.cpu()
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            lat_b1 = {"median_us": ts[len(ts) // 2] * 1e6, "p90_us": ts[int(len(ts) * 0.9)] * 1e6,
+                      "calls": len(ts), "what": "value + dKG/dx at one candidate, device round trip included"}
+
+    # ---- non-degenerate leg: headline sizes, KG > 0 for every pair (workload headline_nd, d = 6)
+    nd = None
+    if args.nd_steps > 0 and args.workload == "headline" and args.precision == "fp64":
+        wn, _, Dn, _, _, _, tpn = setup("headline_nd")
+        en = tpn.run(max(1, args.streams), args.nd_steps, min(args.warmup, 10), bool(args.graph), world)
+        env_us = tpn.plan.time_stage(tpn.Xd, 2, args.profile_reps) * 1e3
+        nd = {"workload": "headline_nd", "value": world * wn.B * args.nd_steps / en, "unit": "KG-evals/s",
+              "steps": args.nd_steps, "ms_per_step": en / args.nd_steps * 1e3, "envelope_us": env_us,
+              "config": {"m": wn.m, "n_train": wn.n_train, "n_disc": Dn.shape[0], "S": wn.S, "B": wn.B, "d": wn.d,
+                         "lengthscales": wn.lengthscales, "outputscales": wn.outputscales, "noise": wn.noise},
+              "batch_stats": batch_stats(tpn.plan, tpn.Xd)}
 
     out = None
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
             cpu = cpu_baseline(model, D, W, X0, args.target, args.cpu_seconds, args.cpu_threads)
+        E = tp.E
         out = {
             "metric": METRIC,
             "value": value,
@@ -332,9 +446,11 @@ def main():
             "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
+            "latency_b1": lat_b1,
             "roofline": roof,
             "forward_roofline": fwd_roof,
-            "batch_stats": pair_stats,
+            "batch_stats": stats,
+            "nondegenerate": nd,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

@@ -73,6 +73,29 @@ def _as_model_state(model) -> ModelListGPState:
     return from_botorch(model)
 
 
+def _fingerprint(obj):
+    """What the fitted state of ``model`` is made of, cheaply: every tensor by (identity, in-place
+    version counter), every other field by value.  The reference reads the model live at every
+    forward (``model.posterior``, discretekg.py:182-185, 275-284); the device state is rebuilt
+    whenever this changes (a refit, new training data, an in-place edit)."""
+    if isinstance(obj, torch.Tensor):
+        return (id(obj), obj._version)
+    if isinstance(obj, ModelListGPState):
+        return tuple(_fingerprint(m) for m in obj.models)
+    if isinstance(obj, SingleTaskGPState):
+        return (_fingerprint(obj.train_x), _fingerprint(obj.train_y), _fingerprint(obj.lengthscale),
+                obj.outputscale, obj.noise, obj.mean_constant, obj.kernel, obj.nu, obj.y_mean, obj.y_std)
+    if isinstance(obj, torch.nn.Module):  # a BoTorch model: parameters, buffers and training data
+        parts = [_fingerprint(t) for t in obj.parameters()] + [_fingerprint(t) for t in obj.buffers()]
+        for sub in getattr(obj, "models", None) or [obj]:
+            parts += [_fingerprint(t) for t in getattr(sub, "train_inputs", ()) or ()]
+            tt = getattr(sub, "train_targets", None)
+            if tt is not None:
+                parts.append(_fingerprint(tt))
+        return tuple(parts)
+    return id(obj)
+
+
 class _ForwardFn(torch.autograd.Function):
     """Device forward; when X requires grad the same C call also returns
     dKG(x_b)/dx_b (dkg_plan_forward_grad), and backward scales it by the
@@ -100,11 +123,11 @@ class DiscreteKnowledgeGradient(_Base):
     def create_with_sobol_sample(cls, model, bounds: Tensor, num_discrete_points: int,
                                  scalarisation_weights: Optional[Tensor] = None,
                                  target_output_ix: Optional[int] = None):
-        """Sobol discretisation (``discretekg.py:33-60``, ``draw_sobol_samples(bounds, N, q=1)``)."""
-        d = bounds.shape[-1]
-        eng = torch.quasirandom.SobolEngine(d, scramble=True)
-        raw = eng.draw(num_discrete_points, dtype=bounds.dtype).to(bounds.device)
-        x_disc = bounds[0] + (bounds[1] - bounds[0]) * raw
+        """Sobol discretisation (``discretekg.py:33-60``): ``draw_sobol_samples(bounds, N, q=1)``,
+        whose scrambling seed is drawn from torch's global RNG, so ``torch.manual_seed`` fixes it."""
+        from .optim import draw_sobol_samples
+
+        x_disc = draw_sobol_samples(bounds, num_discrete_points, q=1).squeeze(1).to(bounds)
         return cls(model, x_disc, scalarisation_weights, target_output_ix)
 
     def __init__(self, model, x_discretisation: Tensor, scalarisation_weights: Optional[Tensor] = None,
@@ -134,9 +157,6 @@ class DiscreteKnowledgeGradient(_Base):
                 f"Expected the last dimension of 'scalarisation_weights' to have one "
                 f"element per objective. Got {scalarisation_weights.shape[-1]=} != "
                 f"{state.num_outputs}=model.num_outputs.")
-        if target_output_ix is not None and not (0 <= int(target_output_ix) < state.num_outputs):
-            raise BotorchTensorDimensionError(
-                f"target_output_ix={target_output_ix} out of range for {state.num_outputs} outputs")
         if precision not in ("fp64", "fp32"):
             raise ValueError(f"precision must be 'fp64' (the reference's) or 'fp32', got {precision!r}")
         # "fp32": the two contractions of the forward in fp32 MFMA (include/dkg.h DKG_PLAN_F32;
@@ -145,10 +165,32 @@ class DiscreteKnowledgeGradient(_Base):
         self.x_discretisation = x_discretisation
         self.scalarisation_weights = scalarisation_weights
         self.target_output_ix = target_output_ix
+        # the reference indexes the outputs with it (posteriors[obj_idx_new], weights[..., obj_idx_new],
+        # discretekg.py:301-321): a negative index counts from the end, one out of range raises
+        # IndexError when the KG is evaluated
+        self._target = None
+        self._target_error = None
+        if target_output_ix is not None:
+            t = int(target_output_ix)
+            if -state.num_outputs <= t < state.num_outputs:
+                self._target = t % state.num_outputs
+            else:
+                self._target_error = IndexError("list index out of range")
+        self._device = device
+        self._fp = _fingerprint(model)
         self._state = DeviceGPState(state, x_discretisation, device)
         self._W = scalarisation_weights.detach().to(self._state.device, torch.double).contiguous()
         self._plan = None
         self._plan_grad = None
+
+    def _refresh(self):
+        """Rebuild the device state if the model changed since it was read (see _fingerprint)."""
+        fp = _fingerprint(self.model)
+        if fp != self._fp:
+            self._state = DeviceGPState(_as_model_state(self.model), self.x_discretisation, self._device)
+            self._plan = None
+            self._plan_grad = None
+            self._fp = fp
 
     def _plan_for(self, B: int, grad: bool = False):
         """The forward plan (with gradient buffers when ``grad``), grown (powers of two) to hold B candidates."""
@@ -159,8 +201,9 @@ class DiscreteKnowledgeGradient(_Base):
                 cap *= 2
             if grad and self.precision == "fp32":
                 raise UnsupportedError("precision='fp32' is forward only; use precision='fp64' for gradients")
-            cur = self._state.plan(self._W, self.target_output_ix, max(cap, 16), grad=grad,
-                                   f32=self.precision == "fp32")
+            if self._target_error is not None:
+                raise self._target_error
+            cur = self._state.plan(self._W, self._target, max(cap, 16), grad=grad, f32=self.precision == "fp32")
             if grad:
                 self._plan_grad = cur
             else:
@@ -177,6 +220,7 @@ class DiscreteKnowledgeGradient(_Base):
             raise RuntimeError(
                 f"Expected X to have last dimension matching 'self.x_discretisation'. "
                 f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
+        self._refresh()
         flat = X.reshape(-1, d)
         Xd = flat.to(self._state.device, torch.double)
         kg = _ForwardFn.apply(Xd, self)
@@ -184,6 +228,7 @@ class DiscreteKnowledgeGradient(_Base):
 
     def forward_pairs(self, X: Tensor) -> Tensor:
         """KG per (candidate, scalarisation): [B, S] (the per-``j`` values of ``:200-233``)."""
+        self._refresh()
         flat = X.reshape(-1, X.shape[-1])
         pairs = torch.empty(flat.shape[0], self._W.shape[0], dtype=torch.double, device=self._state.device)
         self._plan_for(flat.shape[0]).forward(flat, kg_pairs=pairs)

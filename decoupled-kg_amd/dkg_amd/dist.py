@@ -17,6 +17,13 @@ One process per GPU (``torch.distributed``; backend "nccl" is RCCL on ROCm,
 device caches from the same host tensors.  The local evaluation is
 ``DiscreteKnowledgeGradient`` on the rank's device unless ``local_forward``
 is injected (the multi-process CPU tests inject the oracle).
+
+The result is differentiable w.r.t. X on every rank (``optimize_acqf``'s
+L-BFGS-B needs dKG/dX): the exchange is wrapped in autograd functions whose
+backward routes each rank's share of the gradient back to its own
+evaluation, and the gradient w.r.t. X is summed over ranks, so every rank
+receives the full dKG/dX.  Like the forward, ``backward`` is collective:
+every rank must call it with the same incoming gradient.
 """
 
 from __future__ import annotations
@@ -30,6 +37,60 @@ from torch import Tensor
 from .errors import BotorchTensorDimensionError
 
 LocalForward = Callable[[Tensor, Tensor], Tensor]  # (X [B, d], W [S_r, m]) -> KG averaged over W, [B]
+
+
+def _to_comm(t: Tensor, cdev: torch.device) -> Tensor:
+    return t.to(cdev, torch.double).contiguous()
+
+
+class _SumGradOverRanks(torch.autograd.Function):
+    """Identity forward; backward all-reduces (sums) the gradient over the ranks, so each rank's
+    input receives every rank's contribution."""
+
+    @staticmethod
+    def forward(ctx, x, cdev, group):
+        ctx.cdev, ctx.group = cdev, group
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        gc = _to_comm(g, ctx.cdev)
+        dist.all_reduce(gc, op=dist.ReduceOp.SUM, group=ctx.group)
+        return gc.to(g.device, g.dtype), None, None
+
+
+class _AllReduceSum(torch.autograd.Function):
+    """Forward: the sum over ranks of every rank's partial (one all-reduce).  Backward: the
+    incoming gradient (the same on every rank) is the gradient of this rank's partial."""
+
+    @staticmethod
+    def forward(ctx, part, group):
+        out = part.detach().clone()
+        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _AllGather(torch.autograd.Function):
+    """Forward: the ranks' equal-length slices concatenated in rank order (one all-gather).
+    Backward: this rank's slice of the incoming gradient."""
+
+    @staticmethod
+    def forward(ctx, mine, world, rank, group):
+        ctx.rank, ctx.n = rank, mine.shape[0]
+        allv = torch.empty(mine.shape[0] * world, dtype=mine.dtype, device=mine.device)
+        if mine.device.type == "cuda":
+            dist.all_gather_into_tensor(allv, mine.detach().contiguous(), group=group)
+        else:
+            dist.all_gather(list(allv.view(world, -1)), mine.detach().contiguous(), group=group)
+        return allv
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[ctx.rank * ctx.n:(ctx.rank + 1) * ctx.n], None, None, None
 
 
 def shard_range(total: int, rank: int, world: int) -> tuple:
@@ -91,26 +152,28 @@ class ShardedDiscreteKG:
         flat = X.reshape(-1, self.d)
         B = flat.shape[0]
         cdev = self._comm_device(flat)
+        if self.world > 1 and flat.requires_grad:
+            flat = _SumGradOverRanks.apply(flat, cdev, self.group)
         if self.axis == "scalarisations":
-            part = torch.zeros(B, dtype=torch.double, device=cdev)
             n_local = self.w_hi - self.w_lo
             if n_local > 0 and B > 0:
-                part += self._local(flat, self.W[self.w_lo:self.w_hi]).to(cdev, torch.double) * n_local
+                part = self._local(flat, self.W[self.w_lo:self.w_hi]).to(cdev, torch.double) * n_local
+            else:
+                part = torch.zeros(B, dtype=torch.double, device=cdev) + 0.0 * flat.sum().to(cdev, torch.double)
             if self.world > 1:
-                dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+                part = _AllReduceSum.apply(part, self.group)
             out = part / self.S
         else:
             chunk = -(-B // self.world) if B > 0 else 0
             lo, hi = shard_range(B, self.rank, self.world)
-            mine = torch.zeros(chunk, dtype=torch.double, device=cdev)
+            pieces = []
             if hi > lo:
-                mine[: hi - lo] = self._local(flat[lo:hi], self.W).to(cdev, torch.double)
-            if self.world > 1:
-                allv = torch.empty(chunk * self.world, dtype=torch.double, device=cdev)
-                dist.all_gather_into_tensor(allv, mine, group=self.group) if cdev.type == "cuda" else \
-                    dist.all_gather(list(allv.view(self.world, chunk)), mine, group=self.group)
-            else:
-                allv = mine
+                pieces.append(self._local(flat[lo:hi], self.W).to(cdev, torch.double))
+            pad = chunk - (hi - lo)
+            if pad > 0 or not pieces:
+                pieces.append(torch.zeros(pad, dtype=torch.double, device=cdev) + 0.0 * flat.sum().to(cdev, torch.double))
+            mine = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+            allv = _AllGather.apply(mine, self.world, self.rank, self.group) if self.world > 1 else mine
             out = allv[:B]
         return out.to(X.device).reshape(batch_shape)
 

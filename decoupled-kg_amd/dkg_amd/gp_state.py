@@ -152,6 +152,9 @@ class ForwardPlan:
         if self.W.dim() != 2 or self.W.shape[1] != state.m:
             raise ValueError(f"weights must be S x {state.m}")
         self.S = self.W.shape[0]
+        if target is not None and not (0 <= int(target) < state.m):
+            # the C ABI's -1 means "all outputs observed": a negative index never reaches it
+            raise ValueError(f"target must be None (all outputs) or in [0, {state.m}), got {target}")
         self.target = -1 if target is None else int(target)
         self.max_B = int(max_B)
         self.grad = bool(grad)

@@ -48,6 +48,10 @@ WORKLOADS = {
     # well-conditioned, non-degenerate parity variant
     "parity6d": Workload("parity6d", m=2, n_train=128, grid=3, S=8, B=32, d=6,
                          lengthscales=(0.4, 0.7), outputscales=(1.0, 3.0), noise=1e-2),
+    # headline size (n_train 256, N = 1024, S = 16, B = 128) on a GP where the KG of every pair is > 0
+    # (d = 6, Sobol discretisation): the envelope does real work; bench.py's non-degenerate leg
+    "headline_nd": Workload("headline_nd", m=2, n_train=256, grid=0, S=16, B=128, d=6,
+                            lengthscales=(0.25, 0.4), outputscales=(1.0, 1.0), noise=1e-2),
     # BASELINE.json configs[4] (the stress config; computed in fp64 here)
     "stress": Workload("stress", m=3, n_train=1024, grid=64, S=32, B=256,
                        lengthscales=(0.2, 1.8, 0.6), outputscales=(1.0, 50.0, 5.0), noise=1e-3),

@@ -41,8 +41,14 @@ def main():
     kg = acq(X.unsqueeze(-2))
     shapes = [None] * dist.get_world_size()
     dist.all_gather_object(shapes, calls)
+    # gradient through the exchange: every rank gets the full dKG/dX
+    Xr = X.clone().requires_grad_(True)
+    wts = torch.arange(1.0, X.shape[0] + 1.0)
+    (acq(Xr.unsqueeze(-2)) * wts).sum().backward()
+    grads = [None] * dist.get_world_size()
+    dist.all_gather_object(grads, Xr.grad)
     if dist.get_rank() == 0:
-        torch.save({"kg": kg, "calls": shapes}, out)
+        torch.save({"kg": kg, "calls": shapes, "grads": grads}, out)
     dist.destroy_process_group()
 
 

@@ -69,6 +69,16 @@ def test_sharded_matches_unsharded(tmp_path, axis, B, S, target):
         assert sum(c[0][1] for c in calls if c) == S and all(c[0][0] == B for c in calls if c)
     else:
         assert sum(c[0][0] for c in calls if c) == B and all(c[0][1] == S for c in calls if c)
+    # gradient: every rank holds the full d(sum_b w_b KG_b)/dX of the unsharded oracle
+    Xr = X[:B].clone().requires_grad_(True)
+    wts = torch.arange(1.0, B + 1.0, dtype=torch.double)
+    (discrete_kg_batched(om, Xr, D, W[:S], target)[0] * wts).sum().backward()
+    g_ref = Xr.grad
+    for g in res["grads"]:
+        assert g is not None and g.shape == g_ref.shape
+        # the gradient floor of tests/test_gpu_grad.py: 1e-9 of the largest component (cancellation in E - max a)
+        torch.testing.assert_close(g, g_ref, rtol=1e-9, atol=1e-9 * float(g_ref.abs().max()))
+    assert torch.equal(res["grads"][0], res["grads"][1])
 
 
 @pytest.mark.parametrize("mode,steps,every", [("gather", 7, 3), ("gather", 6, 3), ("reduce", 7, 3),

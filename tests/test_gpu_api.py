@@ -1,0 +1,115 @@
+"""The reference's DiscreteKnowledgeGradient surface around the forward (discretekg.py:33-159).
+
+create_with_sobol_sample seeds like draw_sobol_samples (torch's global RNG); set_X_pending
+raises UnsupportedError; target_output_ix indexes the outputs as the reference's
+posteriors[obj_idx_new] does (negative counts from the end, out of range -> IndexError at
+evaluation); the model is read live (a mutated model gives the new model's KG).
+"""
+
+import pytest
+import torch
+
+from dkg_amd import DiscreteKnowledgeGradient
+from dkg_amd.errors import UnsupportedError
+from dkg_amd.model import ModelListGPState, SingleTaskGPState
+from dkg_amd.optim import draw_sobol_samples
+from dkg_amd.synthetic import WORKLOADS, make_problem
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def test_create_with_sobol_sample_is_seeded_by_the_global_rng():
+    model, _, X, W = make_problem(WORKLOADS["small"])
+    bounds = torch.tensor([[0.0, 0.0], [1.0, 1.0]], dtype=torch.double)
+    torch.manual_seed(123)
+    a1 = DiscreteKnowledgeGradient.create_with_sobol_sample(model, bounds, 64, W)
+    torch.manual_seed(123)
+    a2 = DiscreteKnowledgeGradient.create_with_sobol_sample(model, bounds, 64, W)
+    assert torch.equal(a1.x_discretisation, a2.x_discretisation)
+    # the discretisation is draw_sobol_samples(bounds, N, q=1).squeeze(1) (discretekg.py:56-58)
+    torch.manual_seed(123)
+    ref = draw_sobol_samples(bounds, 64, q=1).squeeze(1)
+    assert torch.equal(a1.x_discretisation, ref)
+    assert a1.x_discretisation.shape == (64, 2) and a1.x_discretisation.dtype == bounds.dtype
+    torch.manual_seed(124)
+    a3 = DiscreteKnowledgeGradient.create_with_sobol_sample(model, bounds, 64, W)
+    assert not torch.equal(a1.x_discretisation, a3.x_discretisation)
+    kg1 = a1(X[:8].unsqueeze(-2))
+    kg2 = a2(X[:8].unsqueeze(-2))
+    assert torch.equal(kg1, kg2)
+    # scaled bounds land inside the box
+    b2 = torch.tensor([[-2.0, 1.0], [3.0, 1.5]], dtype=torch.double)
+    a4 = DiscreteKnowledgeGradient.create_with_sobol_sample(model, b2, 32, W, target_output_ix=1)
+    assert bool(((a4.x_discretisation >= b2[0]) & (a4.x_discretisation <= b2[1])).all())
+    assert a4.target_output_ix == 1
+
+
+def test_set_x_pending_raises():
+    model, D, _, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W)
+    with pytest.raises(UnsupportedError, match="does not account for X_pending"):
+        acq.set_X_pending(torch.rand(2, 2, dtype=torch.double))
+    with pytest.raises(UnsupportedError):
+        acq.set_X_pending(None)
+
+
+def test_negative_target_counts_from_the_end():
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    Xb = X[:16].unsqueeze(-2)
+    last = DiscreteKnowledgeGradient(model, D, W, target_output_ix=model.num_outputs - 1)(Xb)
+    neg = DiscreteKnowledgeGradient(model, D, W, target_output_ix=-1)(Xb)
+    assert torch.equal(last, neg)
+    first = DiscreteKnowledgeGradient(model, D, W, target_output_ix=-model.num_outputs)(Xb)
+    assert torch.equal(first, DiscreteKnowledgeGradient(model, D, W, target_output_ix=0)(Xb))
+    full = DiscreteKnowledgeGradient(model, D, W)(Xb)
+    assert not torch.equal(neg, full)  # -1 is the last output, not the full evaluation
+
+
+def test_target_out_of_range_raises_index_error_at_evaluation():
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=model.num_outputs)  # constructs, as the reference
+    with pytest.raises(IndexError):
+        acq(X[:4].unsqueeze(-2))
+
+
+def test_model_is_read_live():
+    """A refit (new hyperparameters), new training data and an in-place edit are all seen by forward."""
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    Xb = X[:16].unsqueeze(-2)
+    acq = DiscreteKnowledgeGradient(model, D, W)
+    before = acq(Xb)
+    # refit: replace an output's hyperparameters
+    m0 = model.models[0]
+    model.models[0] = SingleTaskGPState(m0.train_x, m0.train_y, m0.lengthscale * 1.5, m0.outputscale, m0.noise,
+                                        m0.mean_constant, m0.kernel, m0.nu, m0.y_mean, m0.y_std)
+    after = acq(Xb)
+    fresh = DiscreteKnowledgeGradient(model, D, W)(Xb)
+    assert torch.equal(after, fresh) and not torch.equal(after, before)
+    # in-place edit of the training targets
+    model.models[1].train_y.mul_(2.0)
+    edited = acq(Xb)
+    assert torch.equal(edited, DiscreteKnowledgeGradient(model, D, W)(Xb))
+    assert not torch.equal(edited, after)
+    # unchanged model: the cached state is reused (same values, no rebuild)
+    st = acq._state
+    acq(Xb)
+    assert acq._state is st
+
+
+def test_single_output_model_without_weights():
+    g = torch.Generator().manual_seed(2)
+    Xt = torch.rand(30, 2, generator=g, dtype=torch.double)
+    st = SingleTaskGPState(Xt, torch.sin(4 * Xt[:, 0]), [0.3, 0.4], 1.0, 1e-3)
+    D = torch.rand(50, 2, generator=g, dtype=torch.double)
+    a = DiscreteKnowledgeGradient(st, D)
+    assert torch.equal(a.scalarisation_weights, torch.tensor([[1.0]], dtype=torch.double))
+    b = DiscreteKnowledgeGradient(ModelListGPState(st), D, torch.tensor([[1.0]], dtype=torch.double))
+    Xc = torch.rand(5, 1, 2, generator=g, dtype=torch.double)
+    assert torch.equal(a(Xc), b(Xc))

@@ -438,7 +438,7 @@ def test_concurrent_plans_on_streams_match_single_stream():
     torch.cuda.synchronize()
     main = torch.cuda.current_stream(dev)
     streams = [main] + [torch.cuda.Stream(dev) for _ in range(3)]
-    plans = [base] + [acq._state.plan(acq._W, acq.target_output_ix, base.max_B) for _ in range(3)]
+    plans = [base] + [acq._state.plan(acq._W, acq._target, base.max_B) for _ in range(3)]
     got = torch.full((len(batches), w.B), float("nan"), dtype=torch.double, device=dev)
     for s in streams[1:]:
         s.wait_stream(main)

@@ -1,6 +1,6 @@
 """Aggregate tools/pmc_passes.sh output into per-kernel, per-launch figures.
 
-usage: python tools/pmc_report.py <outdir> <profiles/tag.json>
+usage: python tools/pmc_report.py <outdir> <profiles/tag.json> [profiles/r02/pmc_headline.json]
 
 Per kernel (forward instantiations only): average per launch of every counter,
 per-wave instruction mix, VALU / MFMA busy fractions and HBM bytes.  Units and
@@ -57,6 +57,10 @@ def main():
             r["hbm_bytes_per_launch"] = (2.0 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024.0
             r["fetch_bytes_x2"] = 2.0 * c.get("FETCH_SIZE", 0.0) * 1024.0
             r["write_bytes"] = c.get("WRITE_SIZE", 0.0) * 1024.0
+        if "SQ_ACTIVE_INST_VALU" in c:
+            r["valu_busy_simd_cycles"] = 4.0 * c["SQ_ACTIVE_INST_VALU"]   # summed over waves: SIMD-cycles
+        if "SQ_INSTS_VALU" in c:
+            r["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / w
         if dur.get(name):
             simd_cycles = dur[name] * 1e-6 * CLOCK_GHZ * 1e9 * SIMDS
             if "SQ_ACTIVE_INST_VALU" in c:
@@ -68,6 +72,12 @@ def main():
                 r["mfma_f64_tflops_from_mops"] = c["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512 / (dur[name] * 1e-6) / 1e12
         rep[name] = r
     json.dump(rep, open(dst, "w"), indent=2)
+    if len(sys.argv) > 3:  # the per-launch figures bench.py reads (roofline traffic / VALU busy)
+        keys = ("hbm_bytes_per_launch", "fetch_bytes_x2", "write_bytes", "valu_busy_simd_cycles",
+                "valu_insts_per_wave", "valu_busy_frac", "mfma_busy_frac", "mfma_f64_tflops_from_mops", "avg_us")
+        summ = {n: {k: r[k] for k in keys if k in r} for n, r in rep.items()}
+        summ["_source"] = {"passes": out, "report": dst}
+        json.dump(summ, open(sys.argv[3], "w"), indent=2)
     print(json.dumps({n: {k: v for k, v in r.items() if k != "counters_per_launch"} for n, r in rep.items()},
                      indent=1))
 
