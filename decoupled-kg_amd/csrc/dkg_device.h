@@ -323,24 +323,31 @@ __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane,
     }
   }
   if (!force_walk) {
+    // up to three list walks: at WALK_MARGIN; after an overflow at the tight margin; after a
+    // breakpoint beyond the guard at the margin that covers it
     double rel = WALK_MARGIN;
-    for (int level = 0; level < 2; ++level) {
-      if (f.cnt > ENV_CAP) break;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double cmax;
-      int h;
-      const double kg = walk_small(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
-      if (pst) pst[4] = __builtin_amdgcn_s_memtime();
-      if (uniform(cmax <= rel * WALK_POW2_50)) {
-        *nhull = h;
-        if (pst) pst[7] = (unsigned long long)h | ((unsigned long long)level << 33);
-        return kg;
+    for (int level = 0; level < 3; ++level) {
+      double next = 0.0;
+      if (f.cnt <= ENV_CAP) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double cmax;
+        int h;
+        const double kg = walk_small(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
+        if (pst) pst[4] = __builtin_amdgcn_s_memtime();
+        if (uniform(cmax <= rel * WALK_POW2_50)) {
+          *nhull = h;
+          if (pst) pst[7] = (unsigned long long)h | ((unsigned long long)(level > 0) << 33);
+          return kg;
+        }
+        next = WALK_REFILTER * cmax / WALK_POW2_50;  // a breakpoint beyond the guard
+        if (!uniform(next < WALK_REL_MAX)) break;
+      } else {
+        if (!(rel > WALK_MARGIN_TIGHT)) break;     // overflow at the tight margin
+        next = WALK_MARGIN_TIGHT;
       }
-      // a breakpoint beyond the guard: filter again with the margin that covers it
-      rel = WALK_REFILTER * cmax / WALK_POW2_50;
-      if (!uniform(rel < WALK_REL_MAX) || level == 1) break;
+      rel = next;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -995,7 +1002,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   const int b = blockIdx.x;
   const int g = blockIdx.y;
   const int SW = blockDim.x >> 6;
-  const int lane = threadIdx.x & 63;
+  const int lane_k = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = P->m;  // <= M
   const int N = P->N;
@@ -1073,8 +1080,8 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     if (!STREAM && i < m) {
-      dma_to_lds(mu_src[i], lmu + (size_t)i * SLp, N, wave, SW, lane);
-      if (full || i == target) dma_to_lds(cv_src[i], lcv + (size_t)i * SLp, N, wave, SW, lane);
+      dma_to_lds(mu_src[i], lmu + (size_t)i * SLp, N, wave, SW, lane_k);
+      if (full || i == target) dma_to_lds(cv_src[i], lcv + (size_t)i * SLp, N, wave, SW, lane_k);
     }
   }
   if constexpr (GRAD) {
@@ -1085,9 +1092,9 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
       if (i < m) {
         const int npi = pad16(P->o[i].n);
         const size_t mat = (size_t)P->bpad * npi;
-        dma_to_lds(P->qxrm[i] + (size_t)b * npi, qrow + (size_t)i * NPS, npi, wave, SW, lane);
+        dma_to_lds(P->qxrm[i] + (size_t)b * npi, qrow + (size_t)i * NPS, npi, wave, SW, lane_k);
         for (int dd = 0; dd < d; ++dd)
-          dma_to_lds(P->jq[i] + dd * mat + (size_t)b * npi, jrow + ((size_t)i * d + dd) * NPS, npi, wave, SW, lane);
+          dma_to_lds(P->jq[i] + dd * mat + (size_t)b * npi, jrow + ((size_t)i * d + dd) * NPS, npi, wave, SW, lane_k);
       }
     }
   }
@@ -1186,11 +1193,11 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
     for (int pidx = wave; pidx < m * d; pidx += SW) {
       const int i = pidx / d, dd = pidx % d;
       double acc = 0.0;
-      for (int c = lane; c < NP; c += 64) acc = fma(jrow[((size_t)i * d + dd) * NPS + c], qrow[(size_t)i * NPS + c], acc);
+      for (int c = lane_k; c < NP; c += 64) acc = fma(jrow[((size_t)i * d + dd) * NPS + c], qrow[(size_t)i * NPS + c], acc);
       acc = wave_sum(acc);
-      if (lane == 0) sgv[i * DKG_MAX_DIM + dd] = -2.0 * acc;
+      if (lane_k == 0) sgv[i * DKG_MAX_DIM + dd] = -2.0 * acc;
     }
-    gw[lane] = 0.0;
+    gw[lane_k] = 0.0;
     __syncthreads();
     KST(st, 2);
   }
@@ -1208,6 +1215,11 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
   }
 
   for (int j = g * SW + wave; j < S; j += waves_total) {
+    // The lane index through an opaque move: every lane-dependent address below is computed inside the
+    // loop instead of hoisted out of it and kept live (a wave usually serves a single pair: hoisting
+    // only costs registers).
+    int lane = lane_k;
+    asm volatile("" : "+v"(lane));
     // ---- line coefficients (wave uniform; shared with lines_export_kernel)
     double w[M], wa[M], wb[M];
     double a_off, den;
@@ -1573,7 +1585,7 @@ __global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ 
 
   // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
   if (!GRAD) KST(st, 4);
-  if (lane == 0) s_tail[wave] = wave_acc;
+  if (lane_k == 0) s_tail[wave] = wave_acc;
   __syncthreads();
   if (!GRAD) KST(st, 5);
   if constexpr (GRAD) {

@@ -44,6 +44,9 @@ constexpr double WALK_XGUARD = 1073741824.0;           // 2^30
 constexpr double WALK_POW2_50 = 1125899906842624.0;    // 2^50
 constexpr double WALK_REFILTER = 16.0;
 constexpr double WALK_REL_MAX = 0.00390625;            // 2^-8
+// A list that overflows at WALK_MARGIN is filtered again at the tight margin
+// 2^-30 (guard 2^20) before the walk over all lines is considered.
+constexpr double WALK_MARGIN_TIGHT = 9.313225746154785e-10;  // 2^-30
 
 // psi(c) = E[(Z - c)_+] with the far tail cut to its fp64 value (0 beyond
 // c = 40: exp(-800) underflows), so an infinite breakpoint gives 0, not NaN.
@@ -240,25 +243,31 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
   const int i = lane / G, g = lane % G;
   const int ii = min(i, nc - 1);
   const double bi = sb[ii], ai = sa[ii];
-  double ebj[JL], eaj[JL];
-  int ekj[JL];
-#pragma unroll
-  for (int q = 0; q < JL; ++q) {  // every entry of the lane's share first: one LDS round trip
-    const int jj = min(g + G * q, nc - 1);
-    ebj[q] = sb[jj];
-    eaj[q] = sa[jj];
-    ekj[q] = si[jj];
-  }
+  // the lane's share in chunks of up to four entries, each chunk's loads first (one LDS round trip per
+  // chunk, few registers)
+  constexpr int CH = JL < 4 ? JL : 4;
   double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
   int kb = KEY_NONE, jb = -1;
+#pragma unroll 1
+  for (int q0 = 0; q0 < JL; q0 += CH) {
+    double ebj[CH], eaj[CH];
+    int ekj[CH];
 #pragma unroll
-  for (int q = 0; q < JL; ++q) {
-    const int j = g + G * q;
-    const double bj = ebj[q], aj = eaj[q];
-    const int kj = ekj[q];
-    const double x = (ai - aj) / (bj - bi);
-    if (j < nc && bj > bi && walk_less(x, bj, aj, kj, xb, bb, ab, kb)) {
-      xb = x; bb = bj; ab = aj; kb = kj; jb = j;
+    for (int u = 0; u < CH; ++u) {
+      int jj = min(g + G * (q0 + u), nc - 1);
+      ebj[u] = sb[jj];
+      eaj[u] = sa[jj];
+      ekj[u] = si[jj];
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int j = g + G * (q0 + u);
+      const double bj = ebj[u], aj = eaj[u];
+      const int kj = ekj[u];
+      const double x = (ai - aj) / (bj - bi);
+      if (j < nc && bj > bi && walk_less(x, bj, aj, kj, xb, bb, ab, kb)) {
+        xb = x; bb = bj; ab = aj; kb = kj; jb = j;
+      }
     }
   }
   double xm = xb;

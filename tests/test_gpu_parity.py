@@ -359,13 +359,15 @@ def test_stress_refinement_parity(target):
 
 
 # ---------------------------------------------------------------- fp32 contractions (DKG_PLAN_F32)
-# SURVEY.md 8(d) asks for rel 1e-3 against the fp64 build; measured (tools/f32_check.py) the
-# fp32 rounding of Q_X . Q_D (which cancels against s k(x, z) to ~1e-3 of s) moves meaningful KG values by a
-# median 1e-2..1e-1 relative and by up to ~0.8 on the ill-conditioned s = 50 output, so 1e-3 is NOT met;
-# these tests pin the fp32 mode at what it does deliver: every candidate within 5e-2 of the batch's largest
-# KG, and the median relative difference over the meaningful candidates (KG >= 1e-3 max) below 0.2.
-F32_BATCH_TOL = 5e-2
-F32_MEDIAN_REL = 0.2
+# SURVEY.md 8(d) asks for rel 1e-3 against the fp64 build.  cov = s k(x, z) - Q_X . Q_D loses the factor
+# c = s / (posterior variance) of relative precision to cancellation, so fp32 contractions (unit roundoff
+# 6e-8, n ~ 10^2..10^3 terms) give slopes good to ~c * 1e-6.  Measured (tools/f32_check.py,
+# profiles/r02/r02k_f32_check.txt): c <= 34 (parity6d, headline_nd) -> max rel 1e-4 over the candidates
+# with KG >= 1e-3 of the batch maximum; c ~ 10^3..10^6 (headline, BASELINE configs[4] stress32 with
+# noise 1e-3 s) -> rel 1e-2..1.  The 1e-3 target is therefore attainable only for c <~ 10^2, and these
+# tests hold the fp32 mode to it there; at the stress conditioning it is unattainable in fp32 (DESIGN.md
+# 4.6) and the stress config is computed in fp64.
+F32_RTOL = 1e-3
 
 
 def _f32_vs_f64(workload, target, nX):
@@ -381,23 +383,16 @@ def _f32_vs_f64(workload, target, nX):
     return k32, k64
 
 
-def _check_f32(k32, k64):
+@pytest.mark.parametrize("target", [None, 0, 1])
+@pytest.mark.parametrize("workload,nX", [("parity6d", 32), ("headline_nd", 128)])
+def test_f32_meets_1e3_when_conditioning_allows(workload, nX, target):
+    k32, k64 = _f32_vs_f64(workload, target, nX)
     d = (k32 - k64).abs()
-    assert bool((d <= F32_BATCH_TOL * k64.abs().max()).all()), f"max |d| {float(d.max()):.3e} vs {float(k64.max()):.3e}"
     keep = k64.abs() >= 1e-3 * k64.abs().max()
+    assert int(keep.sum()) >= nX // 4
     rel = (d / k64.abs())[keep]
-    assert float(rel.median()) < F32_MEDIAN_REL, f"median rel {float(rel.median()):.3e}"
-
-
-@pytest.mark.parametrize("target", [None, 0, 2])
-def test_f32_stress_vs_f64(target):
-    """BASELINE.json configs[4] (m=3, n=1024, N=4096, S=32) with fp32 contractions vs the fp64 build."""
-    _check_f32(*_f32_vs_f64("stress32", target, 64))
-
-
-@pytest.mark.parametrize("workload", ["small", "parity6d"])
-def test_f32_small_vs_f64(workload):
-    _check_f32(*_f32_vs_f64(workload, None, 32))
+    assert float(rel.max()) <= F32_RTOL, f"max rel {float(rel.max()):.3e}"
+    assert bool((d <= F32_RTOL * k64.abs().max()).all())
 
 
 def test_f32_refuses_gradient():
