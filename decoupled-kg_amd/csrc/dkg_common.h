@@ -162,11 +162,13 @@ __device__ __forceinline__ double dpp_f64(double v) {
 }
 
 // Returns the partner value of `v` for butterfly step `s` (0..5).
-// Cross-row steps (xor 16, xor 32) use ds_bpermute.  The gfx950
-// v_permlane16_swap / v_permlane32_swap builtins pass an isolated self-test
-// (tests: test_wave_butterfly_primitives) but returned stale partner values
-// inside the envelope walk loop (ROCm 7.2 hipcc; DESIGN.md "Known issues"),
-// so they are not used.
+// Cross-row steps (xor 16, xor 32) use ds_bpermute; the reductions combine
+// the four rows by v_readlane instead (combine_rows).  (gfx950's
+// v_permlane16_swap / v_permlane32_swap write both operands: a lane's partner
+// is the first result element in odd rows / the upper half and the second
+// element elsewhere -- reading only the first returns half the lanes their
+// own value, the "stale partner" of round 1; tools/ubench/permlane.hip,
+// DESIGN.md 4.7.)
 template <int STEP>
 __device__ __forceinline__ double partner_f64(double v) {
   if constexpr (STEP == 0) return dpp_f64<0xB1>(v);        // quad_perm [1,0,3,2]
