@@ -85,6 +85,18 @@ def test_grad_matches_central_differences():
     torch.testing.assert_close(g.cpu(), fd, rtol=1e-4, atol=1e-7 * fd.abs().max().item())
 
 
+@pytest.mark.parametrize("target", [None, 1])
+def test_grad_vs_oracle_headline(target):
+    """Headline workload (n 256, N 1024, S 16): dKG/dx against the oracle's autograd, 32 candidates."""
+    w = WORKLOADS["headline"]
+    model, D, X, W = make_problem(w)
+    X = X[:32]
+    om = to_oracle(model)
+    _, g_ref = oracle_grad(om, X, D, W, target)
+    _, g = native_grad(model, X, D, W, target)
+    assert_grad_close(g, g_ref)
+
+
 def test_grad_headline_batch_consistent():
     """Headline-size batch: gradient rows equal those of the same candidates evaluated alone."""
     model, D, X, W = make_problem(WORKLOADS["headline"])
