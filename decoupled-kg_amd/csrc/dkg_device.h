@@ -977,6 +977,18 @@ __device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, doubl
   }
 }
 
+// Waves per SIMD the register allocation targets.  3 (<= 168 VGPRs) would let
+// a cov or cross_root workgroup share an envelope's CU when several forwards
+// are in flight, but the forward then spills (25 MB of scratch writes per
+// launch, 16.6 us instead of 11.1, 5.8 M instead of 7.4 M KG-evals/s:
+// profiles/r02/r02n_*), so every instantiation keeps 2 (256 VGPRs).
+#ifndef DKG_ENV_FWD_WPE
+#define DKG_ENV_FWD_WPE 2
+#endif
+__host__ __device__ constexpr int env_waves_per_eu(bool grad, bool stream) {
+  return (grad || stream) ? 2 : DKG_ENV_FWD_WPE;
+}
+
 // GRAD: also dKG/dx_b (envelope theorem; include/dkg.h dkg_plan_forward_grad),
 // accumulated into dkg[b x d]; the extra LDS follows the survivor lists.
 // STREAM: no LDS staging of the line data; every pass rebuilds the lines
@@ -985,7 +997,7 @@ template <int MAXL, int M, bool GRAD, bool STREAM>
 // The line data (mu_all, cov_all), the candidate posteriors (var_all, mux_all)
 // and the weights arrive as kernel arguments, so the first DMA issues after a
 // single kernel-argument load instead of a pointer chase through the plan.
-__global__ __launch_bounds__(512) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
                                                        double* __restrict__ pairs_out, int dst,
                                                        const double* __restrict__ xnew, double* __restrict__ dkg,
                                                        const double* __restrict__ mu_all,

@@ -13,7 +13,9 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_size_
 
 from .errors import BotorchTensorDimensionError, DkgNativeError, NotPSDError, UnsupportedError
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdkg.so")
+# DKG_LIB: an alternative build of the same library (A/B measurements by tools/; never set in production)
+LIB_PATH = os.environ.get("DKG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native",
+                                                     "libdkg.so")
 
 ABI_VERSION = 3
 DKG_PLAN_GRAD = 1
