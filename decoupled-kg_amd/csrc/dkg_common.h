@@ -221,6 +221,14 @@ __device__ __forceinline__ double keep_or_qnan(bool c, double v) {
 
 __device__ __forceinline__ double readlane_f64(double v, int l);
 
+// A wave-uniform double moved to SGPRs (v_readfirstlane of both halves), so
+// it takes no VGPRs while it stays live.
+__device__ __forceinline__ double sgpr_f64(double v) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+
+
 // Cross-row combine after DKG_BUTTERFLY_ROW: the four row values by v_readlane
 // (scalar registers, no LDS round trip as the ds_bpermute steps 16/32 take),
 // combined in a fixed order, (r0 op r1) op (r2 op r3): wave-uniform and
@@ -229,7 +237,7 @@ template <class Op>
 __device__ __forceinline__ double combine_rows(double v, Op op) {
   const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
   const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
-  return op(op(r0, r1), op(r2, r3));
+  return sgpr_f64(op(op(r0, r1), op(r2, r3)));  // wave-uniform: held in SGPRs, not VGPRs
 }
 
 // Wave minimum of an int: the four in-row DPP steps, then the four row values by v_readlane.

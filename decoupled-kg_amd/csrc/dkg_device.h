@@ -297,7 +297,7 @@ __device__ __forceinline__ int first_max_index(const double (&la)[MAXL], int nl,
 // line is live across the list walk.  force_walk: test hook (every set takes
 // the walk over all lines).  pst (debug, DKG_DEBUG_STAMPS=2): phase stamps.
 template <int MAXL, class Build>
-__device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
+__device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
                                                 bool force_walk, int* nhull, const WalkOut* out = nullptr,
                                                 unsigned long long* pst = nullptr) {
   FwdEnv f;
@@ -314,7 +314,7 @@ __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane,
         if (lane == 0) out->idx[0] = k;
       }
       *nhull = 1;
-      return 0.0;
+      return EdgeSum{0.0, 0.0, 0.0, false};
     }
     f.cnt = env_compact<MAXL, ENV_CAP>(la, lb, env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR), lane, sb, sa, si);
     if (pst) {
@@ -334,7 +334,7 @@ __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double cmax;
         int h;
-        const double kg = walk_small(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
+        const EdgeSum kg = walk_small(f.cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax, out);
         if (pst) pst[4] = __builtin_amdgcn_s_memtime();
         if (uniform(cmax <= rel * WALK_POW2_50)) {
           *nhull = h;
@@ -359,12 +359,20 @@ __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane,
   }
   double la[MAXL], lb[MAXL];
   build(la, lb);
-  const double kgw = walk_regs<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bT, nhull, out);
+  const EdgeSum kgw = walk_regs<MAXL>(la, lb, nl, lane, f.bL, f.aL, f.bT, nhull, out);
   if (pst) {
     pst[5] = __builtin_amdgcn_s_memtime();
     pst[7] = (unsigned long long)(*nhull) | (1ull << 32);
   }
   return kgw;
+}
+
+// KG_w of register-held lines (env_pair_regs_edges), with the single psi evaluation of its edge terms.
+template <int MAXL, class Build>
+__device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
+                                                bool force_walk, int* nhull, const WalkOut* out = nullptr,
+                                                unsigned long long* pst = nullptr) {
+  return finish_edges(env_pair_regs_edges<MAXL>(build, nl, lane, sb, sa, si, force_walk, nhull, out, pst));
 }
 
 // ---------------------------------------------------------------------------
@@ -864,12 +872,12 @@ __device__ __forceinline__ FwdEnv env_extremes_stream(int nch, int nl, int lane,
 }
 
 template <int MAXL, class Build>
-__device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, double* sb, double* sa, int* si,
+__device__ __forceinline__ EdgeSum env_pair_stream_edges(int nch, int nl, int lane, double* sb, double* sa, int* si,
                                                   double* vreg, bool force_walk, int* nhull, Build&& build) {
   const FwdEnv f = env_extremes_stream<MAXL>(nch, nl, lane, build);
   if (f.status == 1) {
     *nhull = 1;
-    return 0.0;
+    return EdgeSum{0.0, 0.0, 0.0, false};
   }
   const EnvChords ch = env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR);
   int cnt = 0;
@@ -899,7 +907,8 @@ __device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, dou
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double cmax, kg;
+    double cmax;
+    EdgeSum kg;
     int h;
     if (cnt <= 128) kg = walk_small(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
     else if (cnt <= 256) kg = walk_list<4>(cnt, lane, sb, sa, si, f.bL, f.aL, f.bT, &h, &cmax);
@@ -910,6 +919,12 @@ __device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, dou
     }
   }
   return walk_stream<MAXL>(nch, nl, lane, f.bL, f.aL, f.bT, nhull, build);
+}
+
+template <int MAXL, class Build>
+__device__ __forceinline__ double env_pair_stream(int nch, int nl, int lane, double* sb, double* sa, int* si,
+                                                  double* vreg, bool force_walk, int* nhull, Build&& build) {
+  return finish_edges(env_pair_stream_edges<MAXL>(nch, nl, lane, sb, sa, si, vreg, force_walk, nhull, build));
 }
 
 // Line coefficients of one (candidate, scalarisation) pair (discretekg.py:
@@ -985,8 +1000,8 @@ __device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, doubl
 #ifndef DKG_ENV_FWD_WPE
 #define DKG_ENV_FWD_WPE 2
 #endif
-__host__ __device__ constexpr int env_waves_per_eu(bool grad, bool stream) {
-  return (grad || stream) ? 2 : DKG_ENV_FWD_WPE;
+__host__ __device__ constexpr int env_waves_per_eu(int maxl, bool grad, bool stream) {
+  return (grad || stream || maxl > 17) ? 2 : DKG_ENV_FWD_WPE;
 }
 
 // GRAD: also dKG/dx_b (envelope theorem; include/dkg.h dkg_plan_forward_grad),
@@ -997,7 +1012,7 @@ template <int MAXL, int M, bool GRAD, bool STREAM>
 // The line data (mu_all, cov_all), the candidate posteriors (var_all, mux_all)
 // and the weights arrive as kernel arguments, so the first DMA issues after a
 // single kernel-argument load instead of a pointer chase through the plan.
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(MAXL, GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
                                                        double* __restrict__ pairs_out, int dst,
                                                        const double* __restrict__ xnew, double* __restrict__ dkg,
                                                        const double* __restrict__ mu_all,
@@ -1213,7 +1228,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     __syncthreads();
     KST(st, 2);
   }
-  const int waves_total = SW * gridDim.y;
+  // The launch gives every (candidate, scalarisation) pair its own wave (gridDim.y = ceil(S / SW),
+  // envelope_geometry), so the pair "loop" runs at most once: written as a one-shot block, nothing
+  // pair-invariant (the exp / erfc coefficients of psi, lane addresses) is hoisted out of it and kept
+  // live in registers.
   double sv[M], mx0[M], ysd[M], ymu[M], nz[M], os[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
@@ -1226,12 +1244,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     mx0[i] = live ? s_pp[i * 6 + 5] : 0.0;
   }
 
-  for (int j = g * SW + wave; j < S; j += waves_total) {
-    // The lane index through an opaque move: every lane-dependent address below is computed inside the
-    // loop instead of hoisted out of it and kept live (a wave usually serves a single pair: hoisting
-    // only costs registers).
-    int lane = lane_k;
-    asm volatile("" : "+v"(lane));
+  if (const int j = g * SW + wave; j < S) {
+    const int lane = lane_k;
     // ---- line coefficients (wave uniform; shared with lines_export_kernel)
     double w[M], wa[M], wb[M];
     double a_off, den;

@@ -575,7 +575,7 @@ __global__ __launch_bounds__(256) void lines_walk_kernel(const double* __restric
       if (lane == 0) out.idx[0] = k;
     }
   } else {
-    v = walk_stream<MAXL>(nch, L, lane, f.bL, f.aL, f.bT, &h, build, idx ? &out : nullptr);
+    v = finish_edges(walk_stream<MAXL>(nch, L, lane, f.bL, f.aL, f.bT, &h, build, idx ? &out : nullptr));
   }
   if (lane == 0) {
     if (kg) kg[p] = v;

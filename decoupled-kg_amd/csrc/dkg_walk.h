@@ -104,6 +104,22 @@ struct WalkOut {
   int cap;
 };
 
+// The KG edge terms a walk leaves for the single psi evaluation of its caller
+// (finish_edges): `kg` is the part already summed (walks of more than 64
+// steps flush every 64), and each lane with `on` holds one pending edge
+// (b_Q - b_P, +-c).  One psi site per kernel: its exp / erfc coefficients
+// are materialised once, not per walk variant.
+struct EdgeSum {
+  double kg, ec, ed;
+  bool on;
+};
+
+__device__ __forceinline__ double finish_edges(const EdgeSum& e) {
+  // every pending edge beyond psi_edge's cut: its term is exactly 0 (skip exp / erfc)
+  if (ballot(e.on && e.ec <= 40.0) == 0) return e.kg;
+  return e.kg + wave_sum(e.on ? e.ed * psi_edge(e.ec) : 0.0);
+}
+
 // Per-step bookkeeping shared by the walks: the KG edge terms
 // (b_Q - b_P) psi(+-c) (minus sign for edges ending at or left of T), one
 // edge per lane, flushed by a wave sum every 64 steps; the largest |c|; and
@@ -132,10 +148,7 @@ struct WalkAcc {
       ed = 0.0;
     }
   }
-  __device__ __forceinline__ double finish(int lane) {
-    if (h & 63) kg += wave_sum(lane < (h & 63) ? ed * psi_edge(ec) : 0.0);
-    return kg;
-  }
+  __device__ __forceinline__ EdgeSum pending(int lane) const { return {kg, ec, ed, lane < (h & 63)}; }
 };
 
 // Chords L-T and T-R of the candidate filter with the margin: a line (a, b)
@@ -174,11 +187,11 @@ __device__ __forceinline__ uint64_t env_keep_mask(const EnvChords& c, double a, 
 }
 
 // Exact walk over the candidate list (sb, sa, si; nc <= 64 PL entries) from
-// the lowest-index copy of L = (bL, aL).  Returns KG_w (cancellation-free edge
+// the lowest-index copy of L = (bL, aL).  Returns the edge terms (EdgeSum: KG_w after finish_edges, the cancellation-free edge
 // sum); *nhull = envelope lines; *cmax = largest |breakpoint| (the caller
 // checks it against WALK_XGUARD).
 template <int PL>
-__device__ __forceinline__ double walk_list(int nc, int lane, const double* sb, const double* sa, const int* si,
+__device__ __forceinline__ EdgeSum walk_list(int nc, int lane, const double* sb, const double* sa, const int* si,
                                             double bL, double aL, double bT, int* nhull, double* cmax,
                                             const WalkOut* out = nullptr) {
   double eb[PL], ea[PL];
@@ -219,7 +232,7 @@ __device__ __forceinline__ double walk_list(int nc, int lane, const double* sb, 
   }
   *nhull = acc.h + 1;
   *cmax = acc.cmax;
-  return acc.finish(lane);
+  return acc.pending(lane);
 }
 
 // Exact walk over a short candidate list (nc <= R <= 32 entries) by a
@@ -232,15 +245,19 @@ __device__ __forceinline__ double walk_list(int nc, int lane, const double* sb, 
 // steps, :382-401, each step's argmin being exactly the row's).  A row whose
 // minimum is attained by several lanes (concurrent lines, duplicates) is
 // resolved by the full key over those lanes (wave_walk_min).  The KG edge
-// terms are evaluated by the winning lanes in parallel.  Returns KG_w;
+// terms are left on the winning lanes (EdgeSum, evaluated by finish_edges);
 // *cmax = 0 when every breakpoint is within WALK_XGUARD, else the largest
 // |breakpoint|.
 template <int R>
-__device__ __forceinline__ double walk_table(int nc, int lane, const double* sb, const double* sa, const int* si,
+__device__ __forceinline__ EdgeSum walk_table(int nc, int lane, const double* sb, const double* sa, const int* si,
                                              double bL, double aL, double bT, int* nhull, double* cmax,
                                              const WalkOut* out = nullptr) {
   constexpr int G = 64 / R, JL = R / G;
-  const int i = lane / G, g = lane % G;
+  // the row / column split of the lane index inside this instantiation (an opaque copy of the lane:
+  // not hoisted and shared across the table sizes, which would keep their addresses live)
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  const int i = ln / G, g = ln % G;
   const int ii = min(i, nc - 1);
   const double bi = sb[ii], ai = sa[ii];
   // the lane's share in chunks of up to four entries, each chunk's loads first (one LDS round trip per
@@ -307,15 +324,12 @@ __device__ __forceinline__ double walk_table(int nc, int lane, const double* sb,
   const bool won = (win >> lane) & 1;
   *nhull = h + 1;
   *cmax = (ballot(won && !(fabs(xb) <= WALK_XGUARD)) != 0) ? wave_max(won ? fabs(xb) : 0.0) : 0.0;
-  const double ec = (bb <= bT) ? -xb : xb;
-  // every edge beyond psi_edge's cut: KG_w = 0 exactly (skip exp / erfc)
-  if (ballot(won && ec <= 40.0) == 0) return 0.0;
-  return wave_sum(won ? (bb - bi) * psi_edge(ec) : 0.0);
+  return {0.0, (bb <= bT) ? -xb : xb, bb - bi, won};
 }
 
 // Walk over the candidate list: the successor table up to 32 entries, the
 // step-by-step argmin walk beyond (PL list entries per lane).
-__device__ __forceinline__ double walk_small(int nc, int lane, const double* sb, const double* sa, const int* si,
+__device__ __forceinline__ EdgeSum walk_small(int nc, int lane, const double* sb, const double* sa, const int* si,
                                              double bL, double aL, double bT, int* nhull, double* cmax,
                                              const WalkOut* out = nullptr) {
   if (nc <= 8) return walk_table<8>(nc, lane, sb, sa, si, bL, aL, bT, nhull, cmax, out);
@@ -327,7 +341,7 @@ __device__ __forceinline__ double walk_small(int nc, int lane, const double* sb,
 
 // Exact walk over all register lines (line k = lane + 64 t, k < nl).
 template <int MAXL>
-__device__ __forceinline__ double walk_regs(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
+__device__ __forceinline__ EdgeSum walk_regs(const double (&la)[MAXL], const double (&lb)[MAXL], int nl, int lane,
                                             double bL, double aL, double bT, int* nhull,
                                             const WalkOut* out = nullptr) {
   int ks = KEY_NONE;
@@ -357,13 +371,13 @@ __device__ __forceinline__ double walk_regs(const double (&la)[MAXL], const doub
     ac = p.a;
   }
   *nhull = acc.h + 1;
-  return acc.finish(lane);
+  return acc.pending(lane);
 }
 
 // Exact walk over streamed lines: build(c, la, lb) rebuilds chunk c (line
 // k = c * 64 * MAXL + lane + 64 t) every step.
 template <int MAXL, class Build>
-__device__ __forceinline__ double walk_stream(int nch, int nl, int lane, double bL, double aL, double bT, int* nhull,
+__device__ __forceinline__ EdgeSum walk_stream(int nch, int nl, int lane, double bL, double aL, double bT, int* nhull,
                                               Build&& build, const WalkOut* out = nullptr) {
   int ks = KEY_NONE;
   for (int c = nch - 1; c >= 0; --c) {
@@ -403,7 +417,7 @@ __device__ __forceinline__ double walk_stream(int nch, int nl, int lane, double 
     ac = p.a;
   }
   *nhull = acc.h + 1;
-  return acc.finish(lane);
+  return acc.pending(lane);
 }
 
 }  // namespace dkg
