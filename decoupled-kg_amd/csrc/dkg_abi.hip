@@ -42,7 +42,6 @@ struct WsLayout {
   size_t q32[DKG_MAX_OUTPUTS], root32[DKG_MAX_OUTPUTS], disc32[DKG_MAX_OUTPUTS];
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
-  size_t cov[DKG_MAX_OUTPUTS];
   size_t mux_all, var_all, cov_all, mu_all;
   size_t wg_part;
   size_t tickets;
@@ -77,24 +76,26 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
       off = align256(off + (size_t)pad16(std::max(N, 1)) * np * sizeof(float));
     }
   }
-  // contiguous per-output blocks (the envelope stage addresses them from
-  // kernel-argument base pointers): means and variances at the candidates
-  // [m][Bp], the covariance rows [m][B][N], a copy of mu_D [m][N]
+  // contiguous blocks (the envelope stage addresses them from kernel-argument
+  // base pointers): means and variances at the candidates [m][Bp]; the
+  // covariance rows [B][N][rec] and mu_D [N][rec] as line records
+  // (rec = cov_rec(m) doubles per line, outputs side by side)
+  const size_t rec = (size_t)cov_rec(m);
   L.mux_all = off;
   off = align256(off + (size_t)m * Bp * sizeof(double));
   L.var_all = off;
   off = align256(off + (size_t)m * Bp * sizeof(double));
   L.cov_all = off;
-  off = align256(off + (size_t)m * std::max(B, 1) * std::max(N, 1) * sizeof(double));
+  off = align256(off + rec * std::max(B, 1) * std::max(N, 1) * sizeof(double));
   L.mu_all = off;
-  off = align256(off + (size_t)m * std::max(N, 1) * sizeof(double));
+  off = align256(off + rec * std::max(N, 1) * sizeof(double));
   for (int i = 0; i < m; ++i) {
     L.mux[i] = L.mux_all + (size_t)i * Bp * sizeof(double);
     L.var[i] = L.var_all + (size_t)i * Bp * sizeof(double);
-    L.cov[i] = L.cov_all + (size_t)i * std::max(B, 1) * std::max(N, 1) * sizeof(double);
   }
   int sw, split;
   envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split);
+  split = (std::max(S, 1) + sw - 1) / sw;  // instantiations with one pair per wave use the full split
   L.wg_part = off;
   off = align256(off + (size_t)std::max(B, 1) * split * sizeof(double));
   L.tickets = off;
@@ -189,13 +190,12 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
     }
     P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
     P->var[i] = reinterpret_cast<double*>(ws + L.var[i]);
-    P->cov[i] = reinterpret_cast<double*>(ws + L.cov[i]);
   }
   P->mux_all = reinterpret_cast<double*>(ws + L.mux_all);
   P->var_all = reinterpret_cast<double*>(ws + L.var_all);
   P->cov_all = reinterpret_cast<double*>(ws + L.cov_all);
   P->mu_all = reinterpret_cast<double*>(ws + L.mu_all);
-  P->cov_stride = (int64_t)std::max(max_B, 1) * std::max(N, 1);
+  P->cov_stride = (int64_t)std::max(N, 1) * cov_rec(m);
   P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
   P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
@@ -237,8 +237,18 @@ int run_forward(const Plan& h, const Plan* dev, const double* xnew, int B, doubl
 
 size_t plan_slot_bytes() { return align256(sizeof(Plan)); }
 
-// mu_D of every output into the plan's contiguous [m][N] block (stream ordered).
+// mu_D of every output into the plan's line records [N][cov_rec(m)] (stream
+// ordered); the padding components (m < cov_rec(m)) of mu_D and of every
+// covariance row are zeroed here once (the covariance stage writes components
+// < m only), so they enter the line build as 0 with a zero weight.
 int copy_disc_means(const Plan& P, hipStream_t s) {
+  const int rec = cov_rec(P.m);
+  if (rec > P.m && P.N > 0) {
+    const size_t rows = (size_t)std::max(P.max_B, 1) * P.N;
+    int st = hip_check(hipMemsetAsync(P.mu_all, 0, sizeof(double) * rec * P.N, s), "hipMemsetAsync(mu_D)");
+    if (!st) st = hip_check(hipMemsetAsync(P.cov_all, 0, sizeof(double) * rec * rows, s), "hipMemsetAsync(cov)");
+    if (st) return st;
+  }
   for (int i = 0; i < P.m && P.f32; ++i) {
     // F32: fp32 copies of R^T and Q_D for the fp32 contractions
     int st = hip_check(launch_frag_to_f32(P.o[i].root_frag, P.o[i].n, P.o[i].n, P.root32[i], s), "frag_to_f32(R)");
@@ -248,8 +258,8 @@ int copy_disc_means(const Plan& P, hipStream_t s) {
       return st;
   }
   for (int i = 0; i < P.m && P.N > 0; ++i) {
-    int st = hip_check(hipMemcpyAsync(P.mu_all + (size_t)i * P.N, P.o[i].disc_mean, sizeof(double) * P.N,
-                                      hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(mu_D)");
+    int st = hip_check(hipMemcpy2DAsync(P.mu_all + i, sizeof(double) * rec, P.o[i].disc_mean, sizeof(double),
+                                        sizeof(double), P.N, hipMemcpyDeviceToDevice, s), "hipMemcpy2DAsync(mu_D)");
     if (st) return st;
     // GRAD: row-major Q_D for the envelope's per-line row gathers
     if (P.grad && (st = hip_check(launch_unpack_rows(P.o[i].disc_frag, P.N, P.o[i].n, P.qdrm[i], s), "unpack_rows")))

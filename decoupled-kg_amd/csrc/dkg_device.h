@@ -206,6 +206,36 @@ struct FwdEnv {
 // with a NaN intercept, which drop out of every raw min / max (IEEE maxNum)
 // and fail every comparison.  status 1: every |b| < 1e-9 (discretekg.py:363-367)
 // or a single slope (the walk stops at its first line): KG = 0, one line.
+// Wave-uniform max (MAXV) or min of val[t] over the register lines with
+// key[t] == k exactly (-inf / +inf if none).  Per slot one compare into a
+// lane mask; a single hit is read by v_readlane; two or more hits in one slot
+// (exact ties) redo the value as a per-lane fold and a wave reduction.  Keys
+// are never NaN-equal, so the padding lines (NaN intercept and slope) never hit.
+template <int MAXL, bool MAXV>
+__device__ __forceinline__ double tie_extreme(const double (&key)[MAXL], double k, const double (&val)[MAXL]) {
+  double r = MAXV ? -INFINITY : INFINITY;
+  bool multi = false;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    const uint64_t mk = ballot(key[t] == k);
+    if (__builtin_expect(mk != 0, 0)) {  // wave-uniform
+      multi = multi || (mk & (mk - 1)) != 0;
+      const double x = readlane_f64(val[t], (int)__builtin_ctzll(mk));
+      r = MAXV ? fmax(r, x) : fmin(r, x);
+    }
+  }
+  if (__builtin_expect(multi, 0)) {
+    double v = r;
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t)
+      v = MAXV ? fmax_raw(v, keep_or_qnan(key[t] == k, val[t])) : fmin_raw(v, keep_or_qnan(key[t] == k, val[t]));
+    DKG_BUTTERFLY_ROW({ v = MAXV ? fmax_raw(v, partner_f64<S_>(v)) : fmin_raw(v, partner_f64<S_>(v)); })
+    r = MAXV ? combine_rows(v, [](double a, double b) { return fmax(a, b); })
+             : combine_rows(v, [](double a, double b) { return fmin(a, b); });
+  }
+  return sgpr_f64(r);
+}
+
 template <int MAXL>
 __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const double (&lb)[MAXL]) {
   FwdEnv f;
@@ -230,23 +260,40 @@ __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const d
     f.status = 1;
     return f;
   }
-  double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
-#pragma unroll
-  for (int t = 0; t < MAXL; ++t) {
-    aL = fmax_raw(aL, keep_or_qnan(lb[t] == bmin, la[t]));
-    aR = fmax_raw(aR, keep_or_qnan(lb[t] == bmax, la[t]));
-    bT = fmin_raw(bT, keep_or_qnan(la[t] == amax, lb[t]));
-  }
-  DKG_BUTTERFLY_ROW({
-    aL = fmax_raw(aL, partner_f64<S_>(aL));
-    aR = fmax_raw(aR, partner_f64<S_>(aR));
-    bT = fmin_raw(bT, partner_f64<S_>(bT));
-  })
-  f.aL = combine_rows(aL, [](double a, double b) { return fmax(a, b); });
-  f.aR = combine_rows(aR, [](double a, double b) { return fmax(a, b); });
-  f.bT = combine_rows(bT, [](double a, double b) { return fmin(a, b); });
+  // the tie values by lane masks: a slot whose compare hits exactly one lane gives its value by
+  // v_readlane (the usual case: one line attains each extreme); a slot with several hits sends the
+  // value through the per-lane fold and the wave reduction
+  f.aL = tie_extreme<MAXL, true>(lb, bmin, la);
+  f.aR = tie_extreme<MAXL, true>(lb, bmax, la);
+  f.bT = tie_extreme<MAXL, false>(la, amax, lb);
   f.status = 0;
   return f;
+}
+
+// Flat envelope: line T (max a, then min b) lies strictly above every other
+// line, exact copies of T aside, on the whole of [-ENV_FLAT_Z, ENV_FLAT_Z].
+// Then every envelope breakpoint has |c| > ENV_FLAT_Z > 40, every edge term
+// (b_Q - b_P) psi(+-c) is psi_edge's exact 0, and KG_w = 0: the value the
+// walk would return, bit for bit, without the filter and the walk.  Per line
+// the test is fma(Z, |b - bT|, a - aT) <= 2^-40 (a - aT): its three roundings
+// (at most 3u (|a - aT| + Z |b - bT|) <= 6.001u |a - aT| once it passes) stay
+// far inside the 2^-40 |a - aT| it demands, so a passing line other than a
+// copy of T is strictly below T on the interval.  A copy of T gives 0 (passes);
+// a line with a = aT and b != bT gives Z |b - bT| > 0 (fails).  NaN padding
+// lines drop out of the maximum.
+constexpr double ENV_FLAT_Z = 48.0;
+constexpr double ENV_FLAT_REL = 9.094947017729282e-13;  // 2^-40
+
+template <int MAXL>
+__device__ __forceinline__ bool env_flat(const double (&la)[MAXL], const double (&lb)[MAXL], const FwdEnv& f) {
+  double worst = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    const double da = la[t] - f.aT;
+    const double v = fma(ENV_FLAT_Z, fabs(lb[t] - f.bT), da);
+    worst = fmax_raw(worst, fma(-ENV_FLAT_REL, da, v));
+  }
+  return ballot(worst > 0.0) == 0;
 }
 
 // The margin chord filter (EnvChords) over register lines into the list
@@ -299,7 +346,7 @@ __device__ __forceinline__ int first_max_index(const double (&la)[MAXL], int nl,
 template <int MAXL, class Build>
 __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
                                                 bool force_walk, int* nhull, const WalkOut* out = nullptr,
-                                                unsigned long long* pst = nullptr) {
+                                                unsigned long long* pst = nullptr, bool flat_ok = false) {
   FwdEnv f;
   if (pst) pst[0] = __builtin_amdgcn_s_memtime();
   {
@@ -314,6 +361,15 @@ __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, in
         if (lane == 0) out->idx[0] = k;
       }
       *nhull = 1;
+      return EdgeSum{0.0, 0.0, 0.0, false};
+    }
+    if (flat_ok && env_flat<MAXL>(la, lb, f)) {
+      *nhull = 0;  // not walked: KG_w = 0 exactly (env_flat)
+      if (pst) {
+        pst[3] = __builtin_amdgcn_s_memtime();
+        pst[6] = 0;
+        pst[7] = 1ull << 34;
+      }
       return EdgeSum{0.0, 0.0, 0.0, false};
     }
     f.cnt = env_compact<MAXL, ENV_CAP>(la, lb, env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR), lane, sb, sa, si);
@@ -371,8 +427,8 @@ __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, in
 template <int MAXL, class Build>
 __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
                                                 bool force_walk, int* nhull, const WalkOut* out = nullptr,
-                                                unsigned long long* pst = nullptr) {
-  return finish_edges(env_pair_regs_edges<MAXL>(build, nl, lane, sb, sa, si, force_walk, nhull, out, pst));
+                                                unsigned long long* pst = nullptr, bool flat_ok = false) {
+  return finish_edges(env_pair_regs_edges<MAXL>(build, nl, lane, sb, sa, si, force_walk, nhull, out, pst, flat_ok));
 }
 
 // ---------------------------------------------------------------------------
@@ -969,12 +1025,16 @@ __host__ __device__ inline int env_slots(int lines) {
   return lines <= 64 * 2 ? 2 : lines <= 64 * 8 ? 8 : lines <= 64 * 17 ? 17 : 33;
 }
 
-// Stride (doubles) of one staged per-output array: room for the DMA pieces
-// and for every register slot (line k reads index k - 1; indices N ..
-// 64 * slots - 2 hold the padding lines), plus the 2-double front pad.
-__host__ __device__ inline int stage_stride(int N) {
-  const int slots = 64 * env_slots(N + 1);
-  return (stage_len(N) > slots ? stage_len(N) : slots) + 2;
+// Doubles in front of a staged record array: line 0 (the candidate, built from
+// registers) reads record -1 there.
+constexpr int STAGE_FRONT = 8;
+
+// Stride (doubles) of one staged record array [N][rec]: room for the DMA
+// pieces and for every register slot (line k reads record k - 1; records N ..
+// 64 * slots - 2 hold the padding lines), plus the front pad.
+__host__ __device__ inline int stage_stride(int N, int rec) {
+  const int slots = 64 * env_slots(N + 1) * rec;
+  return (stage_len(N * rec) > slots ? stage_len(N * rec) : slots) + STAGE_FRONT;
 }
 
 // Async global -> LDS copy of n doubles (16 B per lane per wave instruction,
@@ -1004,6 +1064,13 @@ __host__ __device__ constexpr int env_waves_per_eu(int maxl, bool grad, bool str
   return (grad || stream || maxl > 17) ? 2 : DKG_ENV_FWD_WPE;
 }
 
+// Forward instantiations whose waves claim further pairs of their candidate
+// (fewer workgroups per candidate than ceil(S / 8): Plan::split); the others
+// keep one pair per wave, whose registers then hold nothing across pairs.
+__host__ __device__ constexpr bool env_claims(int maxl, bool grad, bool stream) {
+  return !grad && !stream && maxl <= 17;
+}
+
 // GRAD: also dKG/dx_b (envelope theorem; include/dkg.h dkg_plan_forward_grad),
 // accumulated into dkg[b x d]; the extra LDS follows the survivor lists.
 // STREAM: no LDS staging of the line data; every pass rebuilds the lines
@@ -1021,7 +1088,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ mux_all,
                                                        const double* __restrict__ wts, long long cov_stride,
                                                        int bpad) {
-  __shared__ double s_tail[16];
+  __shared__ int s_next;  // forward: the next unclaimed pair of this workgroup's group
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space)
   __shared__ double s_pp[DKG_MAX_OUTPUTS * 6];
   __shared__ int s_kind[DKG_MAX_OUTPUTS];  // GRAD: covariance family per output
@@ -1039,6 +1106,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   const bool full = target < 0;
   static_assert(STREAM || MAXL == 2 || MAXL == 8 || MAXL == 17 || MAXL == 33, "slot bucket");
   unsigned long long* st = kst_slot(dst, P, 2);
+  if (__builtin_amdgcn_readfirstlane(P->debug_env) & 2) return;  // ablation: empty envelope stage
   KST_BEGIN(st);
 
   // The DMA sources first, in one scalar-load batch: the LDS-DMA intrinsics
@@ -1047,19 +1115,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   const double* cv_src[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    mu_src[i] = mu_all + (size_t)i * N;
-    cv_src[i] = cov_all + (size_t)i * cov_stride + (size_t)b * N;
+    mu_src[i] = mu_all;
+    cv_src[i] = cov_all + (size_t)b * cov_stride;  // records of candidate b
   }
 
   // LDS: [pad][mu_i over D] per output, [pad][cov_i over D] per output (line
   // k >= 1 reads index k - 1; the pad makes the lane-0 / slot-0 read legal),
   // the weights, then the per-wave survivor lists.
-  const int SLp = STREAM ? 0 : stage_stride(N);
+  constexpr int MP = cov_rec(M);  // doubles per line record
+  const int SLp = STREAM ? 0 : stage_stride(N, MP);
   constexpr int LC = list_cap(STREAM && !GRAD);  // survivor-list capacity per wave
-  double* lmu = smem + 2;
-  double* lcv = lmu + (size_t)M * SLp;
-  double* lw = lcv + (size_t)M * SLp;
-  double* sbuf = lw + ((S * m + 1) & ~1);
+  double* lmu = smem + STAGE_FRONT;
+  double* lcv = lmu + SLp;
+  double* lw = lcv + SLp;
+  double* skg = lw + ((S * m + 1) & ~1);  // KG_j of the group's pairs (summed in j order)
+  double* sbuf = skg + ((S + 1) & ~1);
   // GRAD regions: per-wave index lists, per-wave Q_D accumulators u_i[c], the
   // candidate's q_i and J_i rows, gv / gm / per-wave gradient scratch, x_b.
   const int d = P->d;
@@ -1107,8 +1177,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     if (!STREAM && i < m) {
-      dma_to_lds(mu_src[i], lmu + (size_t)i * SLp, N, wave, SW, lane_k);
-      if (full || i == target) dma_to_lds(cv_src[i], lcv + (size_t)i * SLp, N, wave, SW, lane_k);
+      if (i == 0) {
+        dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
+        dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
+      }
     }
   }
   if constexpr (GRAD) {
@@ -1144,32 +1216,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     }
     if (threadIdx.x < d) g_x = xnew[(size_t)b * d + threadIdx.x];
   }
-  // Padding lines k = N+1 .. 64*MAXL-1 (read at indices N .. 64*MAXL-2) come
-  // out of the branch-free line build as (a = NaN, b = b_0): mu = NaN makes
-  // the intercept NaN whatever the weights, and cov = the candidate's own
-  // variance gives line 0's slope bit for bit (same FMAs, same order).  NaN
-  // drops out of every fmin/fmax (maxNum) and fails every comparison, so the
-  // padding lines are never an extreme, a tie, a survivor or counted, and
-  // the register lines need no per-slot padding selects.  Indices the DMA
-  // does not touch (>= stage_len(N)) are written while it is in flight; the
-  // ones it over-writes with its last piece (N .. stage_len(N)-1, only when N
-  // is not a multiple of 128) after it has landed.
-  const int SLd = STREAM ? 0 : stage_len(N);
-  auto pad_lines = [&](int lo, int hi) {
-    const int np_ = hi - lo;
-    for (int e = threadIdx.x; e < m * np_; e += blockDim.x) {
-      const int i = e / np_, idx = lo + e % np_;
-      lmu[(size_t)i * SLp + idx] = __builtin_nan("");
-      if (full || i == target) lcv[(size_t)i * SLp + idx] = var_all[(size_t)i * bpad + b];
+  // Padding lines k = N+1 .. 64*MAXL-1 (records N .. 64*MAXL-2) come out of
+  // the branch-free line build as (a = NaN, b = NaN): mu = cov = NaN makes
+  // both NaN whatever the weights.  NaN drops out of every fmin/fmax (maxNum)
+  // and fails every comparison, so the padding lines are never an extreme, a
+  // tie, a survivor or counted, and the register lines need no per-slot
+  // padding selects.  Doubles the DMA does not touch (>= stage_len(N * MP))
+  // are written while it is in flight; the ones it over-writes with its last
+  // piece (N * MP .. stage_len(N * MP) - 1) after it has landed.
+  const int SLd = STREAM ? 0 : stage_len(N * MP);
+  const int pad_end = (64 * MAXL - 1) * MP;
+  auto pad_lines = [&](int lo, int hi) {  // doubles lo .. hi-1 of both record arrays
+    for (int e = lo + (int)threadIdx.x; e < hi; e += blockDim.x) {
+      lmu[e] = __builtin_nan("");
+      lcv[e] = __builtin_nan("");
     }
   };
-  if constexpr (!STREAM) pad_lines(max(N, SLd), 64 * MAXL - 1);
+  if constexpr (!STREAM) pad_lines(max(N * MP, SLd), pad_end);
+  // pairs j0 .. j1-1 of the candidate: each wave takes j0 + wave first, then (forward) claims the
+  // next unclaimed one, so the workgroup's waves finish together whatever the pairs cost
+  const int PG = (S + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int j0 = g * PG, j1 = min(S, j0 + PG);
+  if (threadIdx.x == 0) s_next = j0 + SW;
   if (!GRAD) KST(st, 2);  // GRAD stamps: 2 preamble done, 3 filter, 4 hull, 5 gradient flush (first pair)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (!STREAM) {
-    if (SLd > N) {  // uniform
-      pad_lines(N, min(SLd, 64 * MAXL - 1));
+    if (SLd > N * MP) {  // uniform
+      pad_lines(N * MP, min(SLd, pad_end));
       __syncthreads();
     }
   }
@@ -1210,7 +1284,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   // forward: the list's line indices after the vertex arrays (GRAD: sidx)
   int* sif = reinterpret_cast<int*>(sbuf + (size_t)SW * (2 * LC + ((STREAM && !GRAD) ? VREG : 0))) +
              (size_t)wave * LC;
-  double wave_acc = 0.0;
   int* si = nullptr;
   double* gw = nullptr;
   if constexpr (GRAD) {
@@ -1228,10 +1301,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     __syncthreads();
     KST(st, 2);
   }
-  // The launch gives every (candidate, scalarisation) pair its own wave (gridDim.y = ceil(S / SW),
-  // envelope_geometry), so the pair "loop" runs at most once: written as a one-shot block, nothing
-  // pair-invariant (the exp / erfc coefficients of psi, lane addresses) is hoisted out of it and kept
-  // live in registers.
+  // The pair loop: instantiations without env_claims run one pair per wave (gridDim.y = ceil(S / SW)).
   double sv[M], mx0[M], ysd[M], ymu[M], nz[M], os[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
@@ -1244,7 +1314,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     mx0[i] = live ? s_pp[i * 6 + 5] : 0.0;
   }
 
-  if (const int j = g * SW + wave; j < S) {
+  for (int jn = j0 + wave; jn < j1;) {
+    const int j = jn;
     const int lane = lane_k;
     // ---- line coefficients (wave uniform; shared with lines_export_kernel)
     double w[M], wa[M], wb[M];
@@ -1261,7 +1332,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     // STREAM: chunk c of the lines straight from global memory
     auto build_chunk = [&](int c, double (&la)[MAXL], double (&lb)[MAXL]) {
       const int kbase = c * 64 * MAXL;
-      const size_t rowoff = (size_t)b * N;
+      const size_t rowoff = (size_t)b * cov_stride;  // candidate b's records
       const int nmax = max(N, 1) - 1;
 #pragma unroll
       for (int t = 0; t < MAXL; ++t) {
@@ -1271,8 +1342,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           if (i < m) {
-            a = fma(wa[i], mu_all[(size_t)i * N + idx], a);
-            if (full || i == target) bb = fma(wb[i], cov_all[(size_t)i * cov_stride + rowoff + idx], bb);
+            a = fma(wa[i], mu_all[(size_t)idx * MP + i], a);
+            if (full || i == target) bb = fma(wb[i], cov_all[rowoff + (size_t)idx * MP + i], bb);
           }
         }
         la[t] = a;
@@ -1293,36 +1364,39 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     };
     const int nch = (NL + 64 * MAXL - 1) / (64 * MAXL);
     auto build_lines = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
-      const double* mup[M];
+      // line k = lane + 64 t reads record k - 1; outputs in output order (the FMA order of the
+      // reference's weighted sums), two per 16-byte read; components >= m are zero with zero weight
+      const double* mur = lmu + (lane - 1) * MP;
+      const double* cvr = lcv + (lane - 1) * MP;
+      // sum_i c[i] r_i over record r (weights c)
+      auto rec_dot = [&](const double* r, const double (&c)[M], double acc) __attribute__((always_inline)) {
+        if constexpr (MP == 1) {
+          acc = fma(c[0], r[0], acc);
+        } else {
 #pragma unroll
-      for (int i = 0; i < M; ++i) mup[i] = lmu + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
+          for (int q = 0; 2 * q < M; ++q) {
+            const double2 u = *reinterpret_cast<const double2*>(r + 2 * q);
+            acc = fma(c[2 * q], u.x, acc);
+            if (2 * q + 1 < M) acc = fma(c[2 * q + 1], u.y, acc);
+          }
+        }
+        return acc;
+      };
       if (full) {
-        const double* cvp[M];
-#pragma unroll
-        for (int i = 0; i < M; ++i) cvp[i] = lcv + (size_t)((i < m) ? i : 0) * SLp + lane - 1;
 #pragma unroll
         for (int t = 0; t < MAXL; ++t) {
-          double a = a_off, bb = 0.0;
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            a = fma(wa[i], mup[i][64 * t], a);
-            bb = fma(wb[i], cvp[i][64 * t], bb);
-          }
-          la[t] = a;
-          lb[t] = bb;
+          la[t] = rec_dot(mur + 64 * MP * t, wa, a_off);
+          lb[t] = rec_dot(cvr + 64 * MP * t, wb, 0.0);
         }
       } else {
-        const double* cvt = lcv + (size_t)target * SLp + lane - 1;
+        const double* cvt = cvr + target;
         double wbt = 0.0;
 #pragma unroll
         for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
 #pragma unroll
         for (int t = 0; t < MAXL; ++t) {
-          double a = a_off;
-#pragma unroll
-          for (int i = 0; i < M; ++i) a = fma(wa[i], mup[i][64 * t], a);
-          la[t] = a;
-          lb[t] = wbt * cvt[64 * t];
+          la[t] = rec_dot(mur + 64 * MP * t, wa, a_off);
+          lb[t] = wbt * cvt[64 * MP * t];
         }
       }
       {
@@ -1335,7 +1409,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
         la[0] = (lane == 0) ? a : la[0];
         lb[0] = (lane == 0) ? bb : lb[0];
       }
-      // padding lines beyond N: (NaN, b_0) from the padded staging (see above)
+      // padding lines beyond N: (NaN, NaN) from the padded staging (see above)
     };
 
     double kgj;
@@ -1350,7 +1424,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
         f = envelope_filter<MAXL, true>(la, lb, lane, sb, sa, si);
       }
       if (force_walk && f.status == 0) f.status = 2;
-      if (j == g * SW + wave) KST(st, 3);
+      if (j == j0 + wave) KST(st, 3);
       double Vden = den;  // the variance under the square root of the slopes
       if (!full) {
         const double sd2 = ysd[target] * ysd[target];
@@ -1579,9 +1653,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
           auto rebuild = [&](int, double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
           kgj = envelope_walk_stream<MAXL>(1, NL, lane, f, rebuild, visit, f.kL);
         }
-        if (j == g * SW + wave) KST(st, 4);
+        if (j == j0 + wave) KST(st, 4);
         if (nh > 0) flush();
-        if (j == g * SW + wave) KST(st, 5);
+        if (j == j0 + wave) KST(st, 5);
         // - sum_e Dw_e b_e * dV/(2V), - [line 0 attains max a] da_0/dx
         double a0 = a_off;
 #pragma unroll
@@ -1600,18 +1674,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
       auto rebuild = [&](double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
       unsigned long long* pst = (dst == 2 && lane == 0 && (size_t)b * S + j < 2 * KST_WG)
                                     ? P->kstamps + ((size_t)b * S + j) * 8 : nullptr;
-      kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst);
+      // pairs_out also records the envelope size: every pair is walked then
+      kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst,
+                                pairs_out == nullptr && !force_walk);
     }
     if (pairs_out != nullptr && lane == 0) {
       pairs_out[(size_t)b * S + j] = kgj;
       if constexpr (!GRAD) P->hull_pairs[(size_t)b * S + j] = hn;
     }
-    wave_acc += kgj;
+    if (lane == 0) skg[j - j0] = kgj;
+    if constexpr (!env_claims(MAXL, GRAD, STREAM)) {
+      break;  // one pair per wave (launch_env_t): nothing pair-invariant is hoisted and kept live
+    } else {
+      int nx = 0;
+      if (lane == 0) nx = atomicAdd(&s_next, 1);
+      jn = __builtin_amdgcn_readfirstlane(nx);
+    }
   }
 
   // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
   if (!GRAD) KST(st, 4);
-  if (lane_k == 0) s_tail[wave] = wave_acc;
   __syncthreads();
   if (!GRAD) KST(st, 5);
   if constexpr (GRAD) {
@@ -1624,7 +1706,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   }
   if (threadIdx.x == 0) {
     double s = 0.0;
-    for (int w2 = 0; w2 < SW; ++w2) s += s_tail[w2];
+    for (int q = 0; q < j1 - j0; ++q) s += skg[q];
     const int G = gridDim.y;
     if (G == 1) {
       kg[b] = s / (double)S;
@@ -1688,15 +1770,15 @@ __global__ __launch_bounds__(256) void lines_export_kernel(const Plan* __restric
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         if (i < m) {
-          a = fma(wa[i], P->mu_all[(size_t)i * N + k - 1], a);
-          if (full) bb = fma(wb[i], P->cov_all[(size_t)i * P->cov_stride + (size_t)b * N + k - 1], bb);
+          a = fma(wa[i], P->mu_all[(size_t)(k - 1) * cov_rec(M) + i], a);
+          if (full) bb = fma(wb[i], P->cov_all[(size_t)b * P->cov_stride + (size_t)(k - 1) * cov_rec(M) + i], bb);
         }
       }
       if (!full) {
         double wbt = 0.0;
 #pragma unroll
         for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
-        bb = wbt * P->cov_all[(size_t)target * P->cov_stride + (size_t)b * N + k - 1];
+        bb = wbt * P->cov_all[(size_t)b * P->cov_stride + (size_t)(k - 1) * cov_rec(M) + target];
       }
     }
     ao[k] = a;
@@ -1724,7 +1806,9 @@ hipError_t launch_env_t(const EnvLaunch& a) {
     (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);
   const Plan& h = *a.host;
-  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
+  dim3 grid = a.grid;
+  if (!env_claims(MAXL, GRAD, STREAM)) grid.y = (h.S + a.block.x / WAVE - 1) / (a.block.x / WAVE);
+  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights,
                      (long long)h.cov_stride, h.bpad);
   return hipGetLastError();

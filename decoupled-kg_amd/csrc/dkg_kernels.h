@@ -5,6 +5,13 @@
 
 namespace dkg {
 
+// Line records: the posterior means mu_D and a candidate's covariance row are
+// kept [N][cov_rec(m)] (all outputs of a line side by side, zero-padded to a
+// power of two), in global memory and staged as is, so a lane reads two
+// outputs of a line with one 16-byte ds_read_b128 (256 B/clk) instead of
+// per-output 8-byte reads the compiler pairs into ds_read2st64_b64 (128 B/clk).
+__host__ __device__ constexpr int cov_rec(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 4 ? 4 : 8; }
+
 // Everything a forward needs besides the candidates, resident in device memory
 // (written once per (model, discretisation, weights) by dkg_plan_init): the
 // kernels take a pointer to it, so each launch carries ~40 bytes of arguments
@@ -14,7 +21,7 @@ struct Plan {
   int32_t m, d, N, S, target;       // target < 0: all outputs observed
   int32_t max_B, max_np;            // workspace sized for max_B candidates; max n_pad over outputs
   int32_t sw, split;                // envelope geometry: waves per workgroup, workgroups per candidate
-  int32_t debug_env, debug_cov;     // ablation switches (0 in production)
+  int32_t debug_env, debug_cov;     // ablation switches (0 in production; DESIGN.md "Ablations")
   int32_t debug_stamp;              // 1: per-workgroup phase stamps into g_kstamps (0 in production)
   int32_t grad;                     // workspace holds the gradient buffers (DKG_PLAN_GRAD)
   int32_t bpad;                     // pad16(max_B): rows of the fragment-packed candidate buffers
@@ -25,7 +32,6 @@ struct Plan {
   double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
   double* mux[DKG_MAX_OUTPUTS];     // posterior mean at the candidates per output (workspace)
   double* var[DKG_MAX_OUTPUTS];     // noiseless posterior variance s - |Q_X[b]|^2 per output (workspace)
-  double* cov[DKG_MAX_OUTPUTS];     // [B x N] posterior covariance rows per output (workspace)
   double* jq[DKG_MAX_OUTPUTS];      // GRAD: J_g = dK(x,X)/dx_g R, row-major [d][bpad][n_pad] per output
   double* qxrm[DKG_MAX_OUTPUTS];    // GRAD: Q_X = K(x,X) R row-major [bpad][n_pad] per output
   double* qdrm[DKG_MAX_OUTPUTS];    // GRAD: Q_D = K(D,X) R row-major [N][n_pad] per output (written at plan init)
@@ -33,9 +39,9 @@ struct Plan {
   unsigned long long* kstamps;      // debug_stamp: [3][KST_WG][8] phase stamps (device)
   double* mux_all;                  // [m][bpad]  = mux[0..m)
   double* var_all;                  // [m][bpad]  = var[0..m)
-  double* cov_all;                  // [m][cov_stride] = cov[0..m)
-  double* mu_all;                   // [m][N] copy of the outputs' disc_mean
-  int64_t cov_stride;               // max_B * N
+  double* cov_all;                  // [max_B][N][cov_rec(m)] posterior covariance rows, line records (workspace)
+  double* mu_all;                   // [N][cov_rec(m)] the outputs' disc_mean, line records
+  int64_t cov_stride;               // N * cov_rec(m): doubles per candidate in cov_all
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
   int* tickets;                     // [B] arrival counters (split > 2 only)
   float* q32[DKG_MAX_OUTPUTS];      // F32: quad-packed K(x, X) R per output (workspace)

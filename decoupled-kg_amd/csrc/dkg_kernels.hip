@@ -6,6 +6,7 @@
 //   envelope_kernel     lines a_k + b_k z per (candidate, scalarisation), upper
 //                       envelope, closed-form Gaussian expectation, mean over S
 #include "dkg_device.h"
+#include <cstdlib>
 
 namespace dkg {
 
@@ -316,9 +317,10 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
   if (blockIdx.x == 0 && blockIdx.y == 0 && oi == 0) {
     for (int i = threadIdx.x; i < B; i += blockDim.x) {
       kg[i] = 0.0;
-      if (P->split > 2) P->tickets[i] = 0;
+      P->tickets[i] = 0;
     }
   }
+  if (__builtin_amdgcn_readfirstlane(P->debug_cov) & 2) return;  // ablation: empty cross stage
   if constexpr (sizeof(T) == 8) {
     cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
   } else {
@@ -374,6 +376,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   __shared__ __attribute__((aligned(16))) double part[4 * 4 * 64];  // K-half 1 partial tiles
   __shared__ double qpart[4 * 16];
   unsigned long long* st = kst_slot(dst, P, 1);
+  if (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1) return;  // ablation: empty covariance stage
   KST_BEGIN(st);
   const int oi = blockIdx.z;
   const dkg_output& o = P->o[oi];
@@ -459,8 +462,8 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     for (int r = 0; r < 4; ++r) {
       const double sum = (double)accs[r] + part[(tt * 4 + r) * 64 + lane];
       const int b = ti * 16 + mfma_drow<T>(lane, r);
-      if (b < B && k < N)
-        P->cov[oi][(size_t)b * N + k] =
+      if (b < B && k < N)  // line record k of candidate b, component oi (dkg_device.h cov_rec)
+        P->cov_all[(size_t)b * P->cov_stride + (size_t)k * cov_rec(P->m) + oi] =
             o.outputscale * kernel_profile(o.kernel, r2[r]) - sum;
     }
     if (want_var && lane < 16) {
@@ -475,11 +478,11 @@ static int outputs_bucket(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 3 ? 3 :
 
 size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad) {
   const int M = outputs_bucket(m);
-  const size_t staged = stream ? 0 : 2 * (size_t)M * stage_stride(N);
+  const size_t staged = stream ? 0 : 2 * (size_t)stage_stride(N, cov_rec(M));
   const bool refine = stream && !grad;  // streaming forward: long lists + quickhull vertex arrays
   const size_t lc = list_cap(refine);
   // per wave: the list (slopes, intercepts; forward: line indices) and the streaming vertex arrays
-  return ((size_t)2 + staged + ((S * m + 1) & ~1) + (size_t)waves * 2 * lc + (refine ? (size_t)waves * VREG : 0) +
+  return ((size_t)2 + staged + ((S * m + 1) & ~1) + ((S + 1) & ~1) + (size_t)waves * 2 * lc + (refine ? (size_t)waves * VREG : 0) +
           (grad ? 0 : ((size_t)waves * lc + 1) / 2)) * sizeof(double);
 }
 
@@ -511,14 +514,14 @@ __global__ __launch_bounds__(256) void lines_kg_kernel(const double* __restrict_
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p = blockIdx.x * (blockDim.x >> 6) + wave;
   if (p >= P) return;
-  // line k >= L: a NaN intercept (never an extreme, a survivor or a successor)
+  // line k >= L: NaN intercept and slope (never an extreme, a tie, a survivor or a successor)
   auto build = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
 #pragma unroll
     for (int t = 0; t < MAXL; ++t) {
       const int k = lane + 64 * t;
       const int kk = min(k, L - 1);
       la[t] = (k < L) ? a[(size_t)p * L + kk] : __builtin_nan("");
-      lb[t] = b[(size_t)p * L + kk];
+      lb[t] = (k < L) ? b[(size_t)p * L + kk] : __builtin_nan("");
     }
   };
   const int nw = blockDim.x >> 6;
@@ -687,11 +690,16 @@ static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const doubl
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {
   // Up to 8 scalarisation waves of one candidate per workgroup; with S <= 16
   // at most two workgroups per candidate, whose partial sums meet in one
-  // commutative atomic add (no inter-workgroup fences).
+  // commutative atomic add (no inter-workgroup fences).  DKG_ENV_SPLIT
+  // (1 .. ceil(S / 8)) sets fewer workgroups per candidate, whose waves then
+  // claim the candidate's pairs one by one.
   (void)B;
   const int sw = std::max(1, std::min(8, S));
+  const int full = (S + sw - 1) / sw;
+  static const char* env = std::getenv("DKG_ENV_SPLIT");
+  const int want = env ? std::atoi(env) : full;
   *waves_per_wg = sw;
-  *split = (S + sw - 1) / sw;
+  *split = std::max(1, std::min(full, want));
 }
 
 // The envelope launch for the plan's output bucket.

@@ -42,10 +42,11 @@ s = st[ok]
 build = s[:, 1] - s[:, 0]
 ext = s[:, 2] - s[:, 1]
 comp = s[:, 3] - s[:, 2]
-walked = s[:, 4] > s[:, 3]
-walk = np.where(walked, s[:, 4] - s[:, 3], 0)
+walked = (s[:, 4] > s[:, 3]) | (s[:, 5] > s[:, 3])
+walk = np.where(s[:, 5] > s[:, 3], s[:, 5] - s[:, 3], np.where(walked, s[:, 4] - s[:, 3], 0))
 full = (s[:, 7] >> 32) & 1
 refilt = (s[:, 7] >> 33) & 1
+flat = ((s[:, 7] >> 34) & 1).astype(bool)
 hull = s[:, 7] & 0xffffffff
 cnt = s[:, 6]
 
@@ -58,6 +59,9 @@ def q(v):
 
 
 print(f"pairs {P}, with stamps {ok.sum()} (the rest short-circuited)")
+print(f"flat (KG = 0 without a walk): {int(flat.sum())} pairs, compact/test {q(comp[flat])}")
+build, ext, comp, walked, walk, full, refilt, hull, cnt = (v[~flat] for v in (build, ext, comp, walked, walk, full, refilt, hull, cnt))
+print("walked pairs:")
 print("build   ", q(build))
 print("extremes", q(ext))
 print("compact ", q(comp))
