@@ -201,41 +201,47 @@ struct FwdEnv {
   int status;  // 0: list ready, 1: KG = 0 (short-circuit or one slope), 2: overflow
 };
 
+// Wave-uniform max (MAXV) or min of val[t] over the register lines with
+// key[t] == k exactly (-inf / +inf if none): a per-lane fold of compare +
+// select + min/max, all on the VALU (a scalar branch per slot on the compare
+// mask costs more: tools/ubench/env_phases.hip), then the wave reduction.
+// Keys are never NaN-equal, so the padding lines (NaN intercept and slope)
+// never hit.
+template <int MAXL, bool MAXV>
+__device__ __forceinline__ double tie_fold(const double (&key)[MAXL], double k, const double (&val)[MAXL]) {
+  double v = MAXV ? -INFINITY : INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t)
+    v = MAXV ? fmax_raw(v, keep_or_qnan(key[t] == k, val[t])) : fmin_raw(v, keep_or_qnan(key[t] == k, val[t]));
+  DKG_BUTTERFLY_ROW({ v = MAXV ? fmax_raw(v, partner_f64<S_>(v)) : fmin_raw(v, partner_f64<S_>(v)); })
+  return MAXV ? combine_rows(v, [](double a, double b) { return fmax(a, b); })
+              : combine_rows(v, [](double a, double b) { return fmin(a, b); });
+}
+
+// The chord ends' intercepts aL (max a at b = bL) and aR (max a at b = bR),
+// both folds interleaved; needed only once the flat test has failed.
+template <int MAXL>
+__device__ __forceinline__ void env_ends(const double (&la)[MAXL], const double (&lb)[MAXL], FwdEnv& f) {
+  double aL = -INFINITY, aR = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    aL = fmax_raw(aL, keep_or_qnan(lb[t] == f.bL, la[t]));
+    aR = fmax_raw(aR, keep_or_qnan(lb[t] == f.bR, la[t]));
+  }
+  DKG_BUTTERFLY_ROW({
+    aL = fmax_raw(aL, partner_f64<S_>(aL));
+    aR = fmax_raw(aR, partner_f64<S_>(aR));
+  })
+  f.aL = combine_rows(aL, [](double a, double b) { return fmax(a, b); });
+  f.aR = combine_rows(aR, [](double a, double b) { return fmax(a, b); });
+}
+
 // Extremes with their exact ties over register lines: L = min b (tie: max a),
 // R = max b (tie: max a), T = max a (tie: min b).  Padding slots hold lines
 // with a NaN intercept, which drop out of every raw min / max (IEEE maxNum)
 // and fail every comparison.  status 1: every |b| < 1e-9 (discretekg.py:363-367)
 // or a single slope (the walk stops at its first line): KG = 0, one line.
-// Wave-uniform max (MAXV) or min of val[t] over the register lines with
-// key[t] == k exactly (-inf / +inf if none).  Per slot one compare into a
-// lane mask; a single hit is read by v_readlane; two or more hits in one slot
-// (exact ties) redo the value as a per-lane fold and a wave reduction.  Keys
-// are never NaN-equal, so the padding lines (NaN intercept and slope) never hit.
-template <int MAXL, bool MAXV>
-__device__ __forceinline__ double tie_extreme(const double (&key)[MAXL], double k, const double (&val)[MAXL]) {
-  double r = MAXV ? -INFINITY : INFINITY;
-  bool multi = false;
-#pragma unroll
-  for (int t = 0; t < MAXL; ++t) {
-    const uint64_t mk = ballot(key[t] == k);
-    if (__builtin_expect(mk != 0, 0)) {  // wave-uniform
-      multi = multi || (mk & (mk - 1)) != 0;
-      const double x = readlane_f64(val[t], (int)__builtin_ctzll(mk));
-      r = MAXV ? fmax(r, x) : fmin(r, x);
-    }
-  }
-  if (__builtin_expect(multi, 0)) {
-    double v = r;
-#pragma unroll
-    for (int t = 0; t < MAXL; ++t)
-      v = MAXV ? fmax_raw(v, keep_or_qnan(key[t] == k, val[t])) : fmin_raw(v, keep_or_qnan(key[t] == k, val[t]));
-    DKG_BUTTERFLY_ROW({ v = MAXV ? fmax_raw(v, partner_f64<S_>(v)) : fmin_raw(v, partner_f64<S_>(v)); })
-    r = MAXV ? combine_rows(v, [](double a, double b) { return fmax(a, b); })
-             : combine_rows(v, [](double a, double b) { return fmin(a, b); });
-  }
-  return sgpr_f64(r);
-}
-
+// aL and aR are left to env_ends (after the flat test).
 template <int MAXL>
 __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const double (&lb)[MAXL]) {
   FwdEnv f;
@@ -260,12 +266,9 @@ __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const d
     f.status = 1;
     return f;
   }
-  // the tie values by lane masks: a slot whose compare hits exactly one lane gives its value by
-  // v_readlane (the usual case: one line attains each extreme); a slot with several hits sends the
-  // value through the per-lane fold and the wave reduction
-  f.aL = tie_extreme<MAXL, true>(lb, bmin, la);
-  f.aR = tie_extreme<MAXL, true>(lb, bmax, la);
-  f.bT = tie_extreme<MAXL, false>(la, amax, lb);
+  // T's slope here (the flat test needs it); the chord ends' intercepts by env_ends
+  f.bT = tie_fold<MAXL, false>(la, amax, lb);
+  f.aL = f.aR = -INFINITY;
   f.status = 0;
   return f;
 }
@@ -372,6 +375,7 @@ __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, in
       }
       return EdgeSum{0.0, 0.0, 0.0, false};
     }
+    env_ends<MAXL>(la, lb, f);
     f.cnt = env_compact<MAXL, ENV_CAP>(la, lb, env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR), lane, sb, sa, si);
     if (pst) {
       pst[3] = __builtin_amdgcn_s_memtime();

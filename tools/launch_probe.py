@@ -1,5 +1,8 @@
 """Where the forwards-in-flight throughput goes: host launch cost vs GPU time.
 
+Modes: 0 plain launches, 1 one graph forked over the streams, 2 one single-stream
+graph per stream replayed side by side.
+
 Run on the GPU box from the repo root:  python tools/launch_probe.py
 For one headline plan: E = 256 forwards captured as one HIP graph over 1 or 4
 streams, replayed R times; prints the host time spent inside replay() and the
@@ -45,7 +48,27 @@ def probe(ns, graph):
 
     issue()
     torch.cuda.synchronize()
-    if graph:
+    if graph == 2:
+        # one single-stream graph per stream (rows r = i mod ns), replayed side by side
+        gs = []
+        for i in range(ns):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=streams[i] if i else torch.cuda.Stream()):
+                for r in range(i, E, ns):
+                    plans[i].forward_into(Xd, outs[r])
+            gs.append(g)
+        torch.cuda.synchronize()
+
+        def run():
+            cs = torch.cuda.current_stream()
+            for s in streams[1:]:
+                s.wait_stream(cs)
+            for i in range(ns):
+                with torch.cuda.stream(streams[i]):
+                    gs[i].replay()
+            for s in streams[1:]:
+                cs.wait_stream(s)
+    elif graph:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             issue()
@@ -72,6 +95,7 @@ def probe(ns, graph):
           f"GPU {gpu / n * 1e6:7.2f} us/forward, sync tail {tail * 1e3:7.2f} ms", flush=True)
 
 
-for ns in (1, 4):
-    for graph in (False, True):
+modes = [int(v) for v in os.environ.get("PROBE_MODES", "0,1,2").split(",")]
+for ns in [int(v) for v in os.environ.get("PROBE_STREAMS", "1,4").split(",")]:
+    for graph in modes:
         probe(ns, graph)

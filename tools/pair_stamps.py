@@ -73,3 +73,12 @@ for lo, hi in [(0, 8), (8, 16), (16, 32), (32, 64), (64, 129), (129, 10**9)]:
     sel = (cnt >= lo) & (cnt < hi)
     if sel.any():
         print(f"  cnt [{lo},{hi}): {sel.sum():5d} pairs, walk {q(walk[sel & walked])}")
+
+# the slowest pairs (they set the launch's tail): phase cycles, list length, envelope size
+tot = np.where(s[:, 5] > s[:, 3], s[:, 5], np.where(s[:, 4] > s[:, 3], s[:, 4], s[:, 3])) - s[:, 0]
+order = np.argsort(-tot)[:12]
+print("slowest pairs: total / build / extremes / compact / walk cycles, list, hull, flags")
+for r in order:
+    w_ = (s[r, 5] - s[r, 3]) if s[r, 5] > s[r, 3] else (s[r, 4] - s[r, 3] if s[r, 4] > s[r, 3] else 0)
+    print(f"  {tot[r]:6d} {s[r, 1] - s[r, 0]:6d} {s[r, 2] - s[r, 1]:6d} {s[r, 3] - s[r, 2]:6d} {w_:6d}"
+          f"  cnt {s[r, 6]:4d} hull {s[r, 7] & 0xffffffff:3d} flags {s[r, 7] >> 32:#x}")

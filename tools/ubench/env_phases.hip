@@ -1,0 +1,216 @@
+// Cycles per call of the forward envelope's per-pair phases (dkg_device.h), in
+// isolation, at 1 and 2 waves per SIMD (256- and 512-thread workgroups, one
+// workgroup per CU): the line build from staged LDS records, the extremes,
+// the flat test, the margin chord compaction and the exact list walk; and
+// sub-phases of the extremes (the fold, the wave reductions, tie variants).
+// Every iteration re-enters the phase with opaque inputs (asm barriers), so
+// nothing is hoisted or shared between calls.  Lines: 1025 per set (headline
+// N = 1024), m = 2, with one line attaining each extreme.
+//
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../include -I../../decoupled-kg_amd/csrc \
+//            env_phases.hip -o env_phases
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "dkg_device.h"
+
+using namespace dkg;
+
+constexpr int MAXL = 17, M = 2, MP = 2, NLINES = 1025, ITERS = 64;
+
+__device__ __forceinline__ double hash01(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return (x & 0xffffff) * (1.0 / 16777216.0);
+}
+
+// ---- sub-phase variants of env_extremes
+__device__ __forceinline__ double wmin(double v) {
+  DKG_BUTTERFLY_ROW({ v = fmin_raw(v, partner_f64<S_>(v)); })
+  return combine_rows(v, [](double a, double b) { return fmin(a, b); });
+}
+__device__ __forceinline__ double wmax(double v) {
+  DKG_BUTTERFLY_ROW({ v = fmax_raw(v, partner_f64<S_>(v)); })
+  return combine_rows(v, [](double a, double b) { return fmax(a, b); });
+}
+template <bool MX>
+__device__ __forceinline__ double tree(const double (&v)[MAXL]) {
+  double r[16];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) r[t] = MX ? fmax_raw(v[2 * t], v[2 * t + 1]) : fmin_raw(v[2 * t], v[2 * t + 1]);
+#pragma unroll
+  for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+    for (int t = 0; t < w; ++t) r[t] = MX ? fmax_raw(r[2 * t], r[2 * t + 1]) : fmin_raw(r[2 * t], r[2 * t + 1]);
+  return MX ? fmax_raw(r[0], v[16]) : fmin_raw(r[0], v[16]);
+}
+// the tie value of a unique hit by per-lane selects, a mask popcount and one readlane (general
+// fallback when the hits are not unique)
+template <bool MX>
+__device__ __forceinline__ double tie_sel(const double (&key)[MAXL], double k, const double (&val)[MAXL]) {
+  double v = MX ? -INFINITY : INFINITY;
+  uint64_t any = 0;
+  int hits = 0;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    const bool c = key[t] == k;
+    const uint64_t mk = ballot(c);
+    any |= mk;
+    hits += __popcll(mk);
+    v = c ? val[t] : v;
+  }
+  if (__builtin_expect(hits == 1, 1)) return readlane_f64(v, (int)__builtin_ctzll(any));
+  double u = MX ? -INFINITY : INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t)
+    u = MX ? fmax_raw(u, keep_or_qnan(key[t] == k, val[t])) : fmin_raw(u, keep_or_qnan(key[t] == k, val[t]));
+  return MX ? wmax(u) : wmin(u);
+}
+
+template <int PHASE>
+__global__ __launch_bounds__(512) void phase_kernel(double* out, unsigned long long* cyc) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  // staged records: mu [N][2], cov [N][2] (line k reads record k - 1), front pad 8
+  const int SL = stage_stride(NLINES - 1, MP);
+  double* lmu = smem + STAGE_FRONT;
+  double* lcv = lmu + SL;
+  double* lists = lcv + SL;
+  for (int e = threadIdx.x; e < SL - STAGE_FRONT; e += blockDim.x) {
+    const bool pad = e >= (NLINES - 1) * MP;
+    lmu[e] = pad ? __builtin_nan("") : hash01(e * 2654435761u + blockIdx.x);
+    lcv[e] = pad ? __builtin_nan("") : 0.1 * hash01(e * 40503u + 17 + blockIdx.x);
+  }
+  __syncthreads();
+  double* sb = lists + wave * 3 * ENV_CAP;
+  double* sa = sb + ENV_CAP;
+  int* si = reinterpret_cast<int*>(sa + ENV_CAP);
+  double wa[M] = {0.7, 0.3}, wb[M] = {0.49, 0.09};
+  double la[MAXL], lb[MAXL];
+  auto build = [&](double (&ra)[MAXL], double (&rb)[MAXL]) {
+    const double* mur = lmu + (lane - 1) * MP;
+    const double* cvr = lcv + (lane - 1) * MP;
+#pragma unroll
+    for (int t = 0; t < MAXL; ++t) {
+      const double2 u = *reinterpret_cast<const double2*>(mur + 64 * MP * t);
+      const double2 v = *reinterpret_cast<const double2*>(cvr + 64 * MP * t);
+      ra[t] = fma(wa[1], u.y, fma(wa[0], u.x, 0.01));
+      rb[t] = fma(wb[1], v.y, fma(wb[0], v.x, 0.0));
+    }
+    ra[0] = (lane == 0) ? 0.5 : ra[0];
+    rb[0] = (lane == 0) ? 0.2 : rb[0];
+  };
+  build(la, lb);
+  double acc = 0.0;
+  int iacc = 0;
+  const FwdEnv f0 = env_extremes<MAXL>(la, lb);
+  const EnvChords ch0 = env_chords(f0.bL, f0.aL, f0.bT, f0.aT, f0.bR, f0.aR);
+  const int cnt0 = env_compact<MAXL, ENV_CAP>(la, lb, ch0, lane, sb, sa, si);
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < ITERS; ++it) {
+    if constexpr (PHASE == 0) {
+      asm volatile("" : "+v"(wa[0]), "+v"(wb[0]));
+      double ra[MAXL], rb[MAXL];
+      build(ra, rb);
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) acc += ra[t] + rb[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) asm volatile("" : "+v"(la[t]), "+v"(lb[t]));
+      if constexpr (PHASE == 1) {
+        const FwdEnv f = env_extremes<MAXL>(la, lb);
+        acc += f.aL + f.aR + f.bT + f.bL + f.bR + f.aT;
+      } else if constexpr (PHASE == 2) {
+        iacc += env_flat<MAXL>(la, lb, f0) ? 1 : 0;
+      } else if constexpr (PHASE == 3) {
+        iacc += env_compact<MAXL, ENV_CAP>(la, lb, ch0, lane, sb, sa, si);
+      } else if constexpr (PHASE == 4) {
+        double cm;
+        int h;
+        const EdgeSum e = walk_small(min(cnt0, ENV_CAP), lane, sb, sa, si, f0.bL + 0.0 * la[0], f0.aL, f0.bT, &h, &cm);
+        acc += e.ec + e.ed + cm;
+        iacc += h;
+      } else if constexpr (PHASE == 6) {  // pass-1 fold, serial chains
+        double bmin = INFINITY, bmax = -INFINITY, amax = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < MAXL; ++t) {
+          bmin = fmin_raw(bmin, lb[t]);
+          bmax = fmax_raw(bmax, lb[t]);
+          amax = fmax_raw(amax, la[t]);
+        }
+        acc += bmin + bmax + amax;
+      } else if constexpr (PHASE == 7) {  // pass-1 fold, trees
+        acc += tree<false>(lb) + tree<true>(lb) + tree<true>(la);
+      } else if constexpr (PHASE == 8) {  // three wave reductions
+        acc += wmin(lb[0]) + wmax(lb[1]) + wmax(la[2]);
+      } else if constexpr (PHASE == 9) {  // the chord ends (env_ends), after the flat test
+        FwdEnv f = f0;
+        env_ends<MAXL>(la, lb, f);
+        acc += f.aL + f.aR;
+      } else if constexpr (PHASE == 10) {  // fold + reduction x 3 (round-2 tie pass)
+        double aL = -INFINITY, aR = -INFINITY, bT = INFINITY;
+#pragma unroll
+        for (int t = 0; t < MAXL; ++t) {
+          aL = fmax_raw(aL, keep_or_qnan(lb[t] == f0.bL, la[t]));
+          aR = fmax_raw(aR, keep_or_qnan(lb[t] == f0.bR, la[t]));
+          bT = fmin_raw(bT, keep_or_qnan(la[t] == f0.aT, lb[t]));
+        }
+        acc += wmax(aL) + wmax(aR) + wmin(bT);
+      } else if constexpr (PHASE == 11) {  // selects + popcount + readlane x 3
+        acc += tie_sel<true>(lb, f0.bL, la) + tie_sel<true>(lb, f0.bR, la) + tie_sel<false>(la, f0.aT, lb);
+      } else if constexpr (PHASE == 5) {
+        acc += finish_edges(EdgeSum{0.0, 0.5 + 0.01 * la[0], lb[0], lane < 3});
+      }
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc + iacc;
+  if (lane == 0) cyc[blockIdx.x * 8 + wave] = (t1 - t0) / ITERS;
+  if (blockIdx.x == 0 && threadIdx.x == 0) cyc[4096] = cnt0;
+}
+
+template <int PHASE>
+void run(const char* name, double* out, unsigned long long* cyc) {
+  const int SL = stage_stride(NLINES - 1, MP);
+  const size_t lds = (size_t)(STAGE_FRONT + 2 * SL + 8 * 3 * ENV_CAP) * sizeof(double);
+  (void)hipFuncSetAttribute((const void*)phase_kernel<PHASE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  for (int threads : {256, 512}) {
+    (void)hipMemset(cyc, 0, 4100 * sizeof(unsigned long long));
+    hipLaunchKernelGGL(phase_kernel<PHASE>, dim3(256), dim3(threads), lds, 0, out, cyc);
+    if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return; }
+    std::vector<unsigned long long> h(4100);
+    (void)hipMemcpy(h.data(), cyc, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    std::vector<unsigned long long> v;
+    for (int b = 0; b < 256; ++b)
+      for (int w = 0; w < threads / 64; ++w) v.push_back(h[b * 8 + w]);
+    std::sort(v.begin(), v.end());
+    printf("%-10s %d waves/SIMD: cycles per call median %6llu  p90 %6llu  (list %llu)\n", name, threads / 256,
+           v[v.size() / 2], v[v.size() * 9 / 10], h[4096]);
+  }
+}
+
+int main() {
+  double* out;
+  unsigned long long* cyc;
+  if (hipMalloc(&out, 256 * 512 * sizeof(double)) != hipSuccess) return 1;
+  if (hipMalloc(&cyc, 4100 * sizeof(unsigned long long)) != hipSuccess) return 1;
+  run<0>("build", out, cyc);
+  run<1>("extremes", out, cyc);
+  run<2>("flat", out, cyc);
+  run<3>("compact", out, cyc);
+  run<4>("walk", out, cyc);
+  run<5>("psi", out, cyc);
+  run<6>("p1-serial", out, cyc);
+  run<7>("p1-tree", out, cyc);
+  run<8>("reduce x3", out, cyc);
+  run<9>("ends", out, cyc);
+  run<10>("tie-fold", out, cyc);
+  run<11>("tie-select", out, cyc);
+  (void)hipFree(out);
+  (void)hipFree(cyc);
+  return 0;
+}
