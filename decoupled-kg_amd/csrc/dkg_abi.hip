@@ -95,7 +95,6 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
   }
   int sw, split;
   envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split);
-  split = (std::max(S, 1) + sw - 1) / sw;  // instantiations with one pair per wave use the full split
   L.wg_part = off;
   off = align256(off + (size_t)std::max(B, 1) * split * sizeof(double));
   L.tickets = off;

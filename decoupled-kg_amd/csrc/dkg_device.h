@@ -1056,24 +1056,22 @@ __device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, doubl
   }
 }
 
-// Waves per SIMD the register allocation targets.  3 (<= 168 VGPRs) would let
-// a cov or cross_root workgroup share an envelope's CU when several forwards
-// are in flight, but the forward then spills (25 MB of scratch writes per
-// launch, 16.6 us instead of 11.1, 5.8 M instead of 7.4 M KG-evals/s:
-// profiles/r02/r02n_*), so every instantiation keeps 2 (256 VGPRs).
+// Waves per SIMD the register allocation targets.  The forward up to 17
+// slots fits 4 (<= 128 VGPRs: two envelope workgroups, or an envelope and a
+// covariance workgroup, share a CU) without a spill: one pair per wave
+// (nothing carried across pairs), the workgroup-uniform pair coefficients in
+// SGPRs, and psi's exp / rational coefficients read as scalar operands
+// (dkg_common.h psi) instead of libm's constants materialised in VGPRs.
+// Measured steps: 2 waves/SIMD (220 VGPRs) 8.2 M KG-evals/s; 3 (168) 9.07 M;
+// a loop of claimed pairs per wave needed 194 VGPRs at 2 and was slower
+// (profiles/r02/r02y).
 #ifndef DKG_ENV_FWD_WPE
-#define DKG_ENV_FWD_WPE 2
+#define DKG_ENV_FWD_WPE 4
 #endif
-__host__ __device__ constexpr int env_waves_per_eu(int maxl, bool grad, bool stream) {
-  return (grad || stream || maxl > 17) ? 2 : DKG_ENV_FWD_WPE;
+__host__ __device__ constexpr int env_waves_per_eu(int maxl, int m, bool grad, bool stream) {
+  return (grad || stream || maxl > 17) ? 2 : (m >= 8 && maxl > 8) ? 3 : DKG_ENV_FWD_WPE;  // m = 8: 3 spill-free
 }
 
-// Forward instantiations whose waves claim further pairs of their candidate
-// (fewer workgroups per candidate than ceil(S / 8): Plan::split); the others
-// keep one pair per wave, whose registers then hold nothing across pairs.
-__host__ __device__ constexpr bool env_claims(int maxl, bool grad, bool stream) {
-  return !grad && !stream && maxl <= 17;
-}
 
 // GRAD: also dKG/dx_b (envelope theorem; include/dkg.h dkg_plan_forward_grad),
 // accumulated into dkg[b x d]; the extra LDS follows the survivor lists.
@@ -1083,7 +1081,7 @@ template <int MAXL, int M, bool GRAD, bool STREAM>
 // The line data (mu_all, cov_all), the candidate posteriors (var_all, mux_all)
 // and the weights arrive as kernel arguments, so the first DMA issues after a
 // single kernel-argument load instead of a pointer chase through the plan.
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(MAXL, GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(MAXL, M, GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
                                                        double* __restrict__ pairs_out, int dst,
                                                        const double* __restrict__ xnew, double* __restrict__ dkg,
                                                        const double* __restrict__ mu_all,
@@ -1092,7 +1090,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ mux_all,
                                                        const double* __restrict__ wts, long long cov_stride,
                                                        int bpad) {
-  __shared__ int s_next;  // forward: the next unclaimed pair of this workgroup's group
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space)
   __shared__ double s_pp[DKG_MAX_OUTPUTS * 6];
   __shared__ int s_kind[DKG_MAX_OUTPUTS];  // GRAD: covariance family per output
@@ -1237,11 +1234,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     }
   };
   if constexpr (!STREAM) pad_lines(max(N * MP, SLd), pad_end);
-  // pairs j0 .. j1-1 of the candidate: each wave takes j0 + wave first, then (forward) claims the
-  // next unclaimed one, so the workgroup's waves finish together whatever the pairs cost
-  const int PG = (S + (int)gridDim.y - 1) / (int)gridDim.y;
-  const int j0 = g * PG, j1 = min(S, j0 + PG);
-  if (threadIdx.x == 0) s_next = j0 + SW;
+  // pairs j0 .. j1-1 of the candidate, one per wave (gridDim.y = ceil(S / SW), envelope_geometry)
+  const int j0 = g * SW, j1 = min(S, j0 + SW);
   if (!GRAD) KST(st, 2);  // GRAD stamps: 2 preamble done, 3 filter, 4 hull, 5 gradient flush (first pair)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1305,26 +1299,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     __syncthreads();
     KST(st, 2);
   }
-  // The pair loop: instantiations without env_claims run one pair per wave (gridDim.y = ceil(S / SW)).
+  // One pair per wave, written as a one-shot block: nothing pair-invariant (psi's coefficients, lane
+  // addresses) is hoisted out of a loop and kept live in registers.
   double sv[M], mx0[M], ysd[M], ymu[M], nz[M], os[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const bool live = i < m;
-    ysd[i] = live ? s_pp[i * 6 + 0] : 1.0;
-    ymu[i] = live ? s_pp[i * 6 + 1] : 0.0;
-    nz[i] = live ? s_pp[i * 6 + 2] : 0.0;
-    os[i] = live ? s_pp[i * 6 + 3] : 0.0;
-    sv[i] = live ? s_pp[i * 6 + 4] : 0.0;
-    mx0[i] = live ? s_pp[i * 6 + 5] : 0.0;
+    // workgroup-uniform: kept in SGPRs across the pair loop
+    ysd[i] = sgpr_f64(live ? s_pp[i * 6 + 0] : 1.0);
+    ymu[i] = sgpr_f64(live ? s_pp[i * 6 + 1] : 0.0);
+    nz[i] = sgpr_f64(live ? s_pp[i * 6 + 2] : 0.0);
+    os[i] = sgpr_f64(live ? s_pp[i * 6 + 3] : 0.0);
+    sv[i] = sgpr_f64(live ? s_pp[i * 6 + 4] : 0.0);
+    mx0[i] = sgpr_f64(live ? s_pp[i * 6 + 5] : 0.0);
   }
 
-  for (int jn = j0 + wave; jn < j1;) {
-    const int j = jn;
+  if (const int j = j0 + wave; j < j1) {
     const int lane = lane_k;
     // ---- line coefficients (wave uniform; shared with lines_export_kernel)
     double w[M], wa[M], wb[M];
     double a_off, den;
     pair_coefs<M>(lw + j * m, m, full, target, ysd, ymu, nz, sv, w, wa, wb, a_off, den);
+#pragma unroll
+    for (int i = 0; i < M; ++i) {  // wave-uniform: SGPRs, not VGPRs, while the lines are live
+      w[i] = sgpr_f64(w[i]);
+      wa[i] = sgpr_f64(wa[i]);
+      wb[i] = sgpr_f64(wb[i]);
+    }
+    a_off = sgpr_f64(a_off);
+    den = sgpr_f64(den);
     // ---- lines: slot t of lane l is line k = l + 64 t (k = 0: the candidate).
     // Branch-free bodies (one LDS read stream per array, no per-slot waits):
     // unused output slots read output 0 with a zero weight.  Rebuilt from the
@@ -1687,13 +1690,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
       if constexpr (!GRAD) P->hull_pairs[(size_t)b * S + j] = hn;
     }
     if (lane == 0) skg[j - j0] = kgj;
-    if constexpr (!env_claims(MAXL, GRAD, STREAM)) {
-      break;  // one pair per wave (launch_env_t): nothing pair-invariant is hoisted and kept live
-    } else {
-      int nx = 0;
-      if (lane == 0) nx = atomicAdd(&s_next, 1);
-      jn = __builtin_amdgcn_readfirstlane(nx);
-    }
   }
 
   // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
@@ -1810,9 +1806,7 @@ hipError_t launch_env_t(const EnvLaunch& a) {
     (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);
   const Plan& h = *a.host;
-  dim3 grid = a.grid;
-  if (!env_claims(MAXL, GRAD, STREAM)) grid.y = (h.S + a.block.x / WAVE - 1) / (a.block.x / WAVE);
-  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
+  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights,
                      (long long)h.cov_stride, h.bpad);
   return hipGetLastError();

@@ -354,15 +354,19 @@ size_t cross_root_lds_bytes(int np, int d) {
 
 // ---------------------------------------------------------------------------
 // posterior_cov_kernel: cov[b][k] = s k(x_b, D_k) - sum_l Q[b][l] Q_D[k][l]
-// One workgroup (8 waves) per 32 x 32 block = 2 x 2 output tiles of one
-// output; wave w computes tile (w & 3) over K-half (w >> 2).  The two waves
-// of a tile that share a K-half of an operand tile read it at the same time,
-// so a CU fetches each operand byte about once (L1); every load is a 16-byte
+// One workgroup (8 waves, 2 per SIMD) per 32 x 32 block = 2 x 2 output
+// tiles of one output; wave w computes tile (w % 4) over K-half (w / 4).
+// Waves that share an operand tile and a K-half read it at the same time, so
+// a CU fetches each operand byte about once (L1); every load is a 16-byte
 // pair (two k-blocks).  K-halves meet in LDS; the K-half-0 wave evaluates
 // the kernel epilogue and stores.  Tiles with tk == 0 also produce the
-// candidates' own variances s - |Q_X[b]|^2.
+// candidates' own variances s - |Q_X[b]|^2.  At <= 128 VGPRs two blocks share
+// a CU: a 64 x 32 block of 16 waves (4 per SIMD) halves the workgroups but
+// holds the CU alone, and its forwards-in-flight throughput was lower
+// (profiles/r02/r02x).
 constexpr int PC_WAVES = 8;
-constexpr int PC_P = 8;  // 16-byte pairs per operand per load batch (16 k-blocks)
+constexpr int PC_RB = 2;  // 16-row tiles per workgroup (32 candidates); 2 column tiles (32 lines)
+constexpr int PC_P = 8;  // 16-byte words per operand per load batch (16 k-blocks)
 
 // T = float (DKG_PLAN_F32): the contraction Q_X . Q_D in fp32 (quad-packed
 // operands, v_mfma_f32_16x16x4_f32); the kernel term, the subtraction and the
@@ -373,8 +377,9 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
                                                                          int dst) {
   constexpr int QW = kpack<T>();
   typedef typename AccT<T>::type acc_t;
-  __shared__ __attribute__((aligned(16))) double part[4 * 4 * 64];  // K-half 1 partial tiles
-  __shared__ double qpart[4 * 16];
+  constexpr int NT = 2 * PC_RB;  // output tiles per workgroup
+  __shared__ __attribute__((aligned(16))) double part[NT * 4 * 64];  // K-half 1 partial tiles
+  __shared__ double qpart[NT * 16];
   unsigned long long* st = kst_slot(dst, P, 1);
   if (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1) return;  // ablation: empty covariance stage
   KST_BEGIN(st);
@@ -383,8 +388,8 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   const int N = P->N;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tt = wave & 3, half = wave >> 2;
-  const int ti = 2 * blockIdx.y + (tt >> 1);
+  const int tt = wave % NT, half = wave / NT;
+  const int ti = PC_RB * blockIdx.y + (tt >> 1);
   const int tk = 2 * blockIdx.x + (tt & 1);
   const int KB = pad16(o.n) / 4;
   const bool have_d = N > 0;
@@ -404,9 +409,25 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     qd = P->disc32[oi];
   }
 
-  // epilogue operands first (row b = 16 ti + (l >> 4) + 4 r, column k = 16 tk + (l & 15))
+  // The first batch of contraction operands is loaded first and the epilogue's
+  // inputs after it, so both memory round trips overlap (row b = 16 ti + (l >> 4) + 4 r,
+  // column k = 16 tk + (l & 15)).
   const int d = P->d;
   const int k = tk * 16 + (lane & 15);
+  // disc_frag tile 0 exists only when N == 0: the N == 0 variance-only
+  // wave reads its own Q_X tile as a stand-in (multiplied by 0 below)
+  const T* dsrc = have_d ? qd : qx;
+  const int dt = have_d ? tk : ti;
+  T va[PC_P][QW], vd[PC_P][QW];
+  auto load_batch = [&](int pb) {
+#pragma unroll
+    for (int u = 0; u < PC_P; ++u) {
+      const int j = min(pb + u, p1 - 1);
+      frag_word<T>(qx, ti, j, lane, KB, va[u]);
+      frag_word<T>(dsrc, dt, j, lane, KB, vd[u]);
+    }
+  };
+  if (live && p0 < p1) load_batch(p0);
   double r2[4] = {0.0, 0.0, 0.0, 0.0};
   if (half == 0) {  // wave-uniform; P->disc is valid even when N == 0 (plan init)
     const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
@@ -421,17 +442,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   double qsq = 0.0;  // lane l: sum over this wave's k of Q_X[16 ti + (l & 15)][k]^2
   if (live) {
     for (int pb = p0; pb < p1; pb += PC_P) {
-      T va[PC_P][QW], vd[PC_P][QW];
-      // disc_frag tile 0 exists only when N == 0: the N == 0 variance-only
-      // wave reads its own Q_X tile as a stand-in (multiplied by 0 below)
-      const T* dsrc = have_d ? qd : qx;
-      const int dt = have_d ? tk : ti;
-#pragma unroll
-      for (int u = 0; u < PC_P; ++u) {
-        const int j = min(pb + u, p1 - 1);
-        frag_word<T>(qx, ti, j, lane, KB, va[u]);
-        frag_word<T>(dsrc, dt, j, lane, KB, vd[u]);
-      }
+      if (pb != p0) load_batch(pb);
 #pragma unroll
       for (int u = 0; u < PC_P; ++u) {
         const bool in = pb + u < p1 && have_d;
@@ -675,7 +686,7 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
                        h.debug_stamp);
     return hipGetLastError();
   }
-  dim3 grid(std::max(1, (h.N + 31) / 32), (B + 31) / 32, h.m);
+  dim3 grid(std::max(1, (h.N + 31) / 32), (B + 16 * PC_RB - 1) / (16 * PC_RB), h.m);
   hipLaunchKernelGGL((posterior_cov_kernel<DM, T>), grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B, h.debug_stamp);
   return hipGetLastError();
 }
@@ -688,18 +699,13 @@ static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const doubl
 }
 
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {
-  // Up to 8 scalarisation waves of one candidate per workgroup; with S <= 16
-  // at most two workgroups per candidate, whose partial sums meet in one
-  // commutative atomic add (no inter-workgroup fences).  DKG_ENV_SPLIT
-  // (1 .. ceil(S / 8)) sets fewer workgroups per candidate, whose waves then
-  // claim the candidate's pairs one by one.
+  // Up to 8 scalarisation waves of one candidate per workgroup, one pair per
+  // wave; with S <= 16 at most two workgroups per candidate, whose partial
+  // sums meet in one commutative atomic add (no inter-workgroup fences).
   (void)B;
   const int sw = std::max(1, std::min(8, S));
-  const int full = (S + sw - 1) / sw;
-  static const char* env = std::getenv("DKG_ENV_SPLIT");
-  const int want = env ? std::atoi(env) : full;
   *waves_per_wg = sw;
-  *split = std::max(1, std::min(full, want));
+  *split = (S + sw - 1) / sw;
 }
 
 // The envelope launch for the plan's output bucket.

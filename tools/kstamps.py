@@ -51,7 +51,8 @@ for k in range(3):
           f" us  (span {rt1.max() - rt0.min():.2f} us)")
     cyc = s[:, 6] - s[:, 1]
     rate = np.median(cyc / np.maximum(1e-9, (s[:, 7] - s[:, 0]) / 100.0))
-    print(f"   s_memtime rate ~{rate:.0f} cycles/us; WG lifetime median {np.median(cyc):.0f} max {cyc.max()} cycles")
+    print(f"   s_memtime rate ~{rate:.0f} cycles/us; WG lifetime median {np.median(cyc):.0f} mean {cyc.mean():.0f}"
+          f" max {cyc.max()} cycles; sum {cyc.sum() / rate:.0f} WG-us = {cyc.sum() / rate / 256:.2f} us on 256 CUs")
     marks = [1, 2, 3, 4, 5, 6]
     for i in range(5):
         a, b = marks[i], marks[i + 1]
