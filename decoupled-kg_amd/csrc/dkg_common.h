@@ -293,53 +293,71 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 // (their coefficients materialised in VGPRs); these coefficients are read
 // from constant memory through an opaque pointer (horner), one scalar operand
 // per FMA.
-static __constant__ double PSI_PA[9] = {1.0, 2.796346091120482, 4.476998603222499, 4.347508891535361, 2.7165796377890157, 1.0037192400095971, 0.17325326370833247, -4.618396778934904e-05, 3.3360288569271207e-06};
-static __constant__ double PSI_QA[9] = {1.0, 7.809602640382476, 27.628540187254945, 58.0088790797422, 79.3523289449324, 72.75170128287581, 43.91331216452371, 16.08152617590387, 2.7670522859865594};
-static __constant__ double PSI_PB[7] = {0.9981308338834465, 3.6598787850514367, 4.641485909810474, 2.472764850018868, 0.5303020141112789, 0.034608494860324725, 0.00012399724831674248};
-static __constant__ double PSI_QB[7] = {1.0, 3.8515503731650442, 5.30522462058383, 3.263540634985728, 0.913625609211908, 0.10482146071245484, 0.003532980749196329};
 
-// Horner over a coefficient table read through an opaque pointer: the
-// coefficients are scalar loads at the use (SGPR operands of the FMAs), never
-// constants the compiler materialises early in VGPRs.
+// psi's coefficients in one constant table (offsets PSI_OFF_*): exp's Taylor
+// terms 1/k! (k = 0..13), then PA, QA (x < 4) and PB, QB (x >= 4) from
+// tools/fit_psi.py.
+static __constant__ double PSI_TAB[46] = {
+    // EXP_TAYLOR
+    1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664, 0.008333333333333333, 0.001388888888888889, 0.0001984126984126984, 2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07, 2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10,
+    // PSI_PA
+    1.0, 2.796346091120482, 4.476998603222499, 4.347508891535361, 2.7165796377890157, 1.0037192400095971, 0.17325326370833247, -4.618396778934904e-05, 3.3360288569271207e-06,
+    // PSI_QA
+    1.0, 7.809602640382476, 27.628540187254945, 58.0088790797422, 79.3523289449324, 72.75170128287581, 43.91331216452371, 16.08152617590387, 2.7670522859865594,
+    // PSI_PB
+    0.9981308338834465, 3.6598787850514367, 4.641485909810474, 2.472764850018868, 0.5303020141112789, 0.034608494860324725, 0.00012399724831674248,
+    // PSI_QB
+    1.0, 3.8515503731650442, 5.30522462058383, 3.263540634985728, 0.913625609211908, 0.10482146071245484, 0.003532980749196329,
+};
+constexpr int PSI_OFF_EXP = 0;
+constexpr int PSI_OFF_PA = 14;
+constexpr int PSI_OFF_QA = 23;
+constexpr int PSI_OFF_PB = 32;
+constexpr int PSI_OFF_QB = 39;
+
+// Horner over N coefficients at c (c[0] the constant term).
 template <int N>
-__device__ __forceinline__ double horner(const double (&tab)[N], double v) {
-  const double* c = tab;
-  asm volatile("" : "+s"(c));
+__device__ __forceinline__ double horner(const double* c, double v) {
   double r = c[N - 1];
 #pragma unroll
   for (int i = N - 2; i >= 0; --i) r = fma(r, v, c[i]);
   return r;
 }
 
-// 1/k!, k = 0..13: exp on |r| <= ln2 / 2 to ~4e-18 truncation
-static __constant__ double EXP_TAYLOR[14] = {1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664,
-                                             0.008333333333333333, 0.001388888888888889, 0.0001984126984126984,
-                                             2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07,
-                                             2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10};
+// The table through an opaque pointer: the coefficients are scalar loads at
+// the use (SGPR operands of the FMAs), never constants the compiler
+// materialises early in VGPRs.
+__device__ __forceinline__ const double* psi_tab() {
+  const double* c = PSI_TAB;
+  asm volatile("" : "+s"(c));
+  return c;
+}
 
 // exp(y) for y <= 0 (0 below -760, where it underflows): y = k ln2 + r with
-// the reduction in two FMAs (ln2 to 2^-106), the Taylor polynomial through
-// the opaque table, v_ldexp (gradual underflow).  Relative error ~1e-16.
-__device__ __forceinline__ double exp_nonpos(double y) {
+// the reduction in two FMAs (ln2 to 2^-106), the Taylor polynomial (terms to
+// k = 13: truncation ~4e-18 on |r| <= ln2 / 2) from the table, v_ldexp
+// (gradual underflow).  Relative error ~1e-16.
+__device__ __forceinline__ double exp_nonpos(double y, const double* tab) {
   if (!(y > -760.0)) return (y != y) ? y : 0.0;
   const double k = rint(y * 1.4426950408889634);
   double r = fma(-k, 0.6931471805599453, y);
   r = fma(-k, 2.3190468138462996e-17, r);
-  return ldexp(horner(EXP_TAYLOR, r), (int)k);
+  return ldexp(horner<14>(tab + PSI_OFF_EXP, r), (int)k);
 }
 
 __device__ __forceinline__ double psi(double c) {
+  const double* tab = psi_tab();
   const double x = fabs(c);
   const double x2 = x * x, x2l = fma(x, x, -x2);  // x^2 = x2 + x2l exactly
-  const double e = 0.3989422804014327 * exp_nonpos(-0.5 * x2) * fma(-0.5, x2l, 1.0);
+  const double e = 0.3989422804014327 * exp_nonpos(-0.5 * x2, tab) * fma(-0.5, x2l, 1.0);
   double g;
   if (x < 4.0) {
     const double v = 0.25 * x;
-    g = horner(PSI_PA, v) / horner(PSI_QA, v);
+    g = horner<9>(tab + PSI_OFF_PA, v) / horner<9>(tab + PSI_OFF_QA, v);
   } else {
     const double s = 1.0 / (x * x);
     const double u = (s - 0.000625) * 16.161616161616163;  // (s - 1/1600) / (1/16 - 1/1600)
-    g = s * (horner(PSI_PB, u) / horner(PSI_QB, u));
+    g = s * (horner<7>(tab + PSI_OFF_PB, u) / horner<7>(tab + PSI_OFF_QB, u));
   }
   const double r = e * g;
   return (c < 0.0) ? r + x : r;

@@ -101,16 +101,40 @@ __device__ __forceinline__ void frag_word(const T* __restrict__ base, int tile, 
 }
 
 // ---------------------------------------------------------------------------
-// cross_root_kernel: one workgroup per (16-row tile ti, tile pair p, output).
-// The pair is (p, T-1-p) of 16-column tiles of Q = K_x R; R upper triangular
-// means tile tj only needs k-blocks kb < 4(tj+1), so pairing the shortest
-// with the longest tile balances the MFMA count across workgroups.  The
-// training inputs are staged in LDS, the K(x, X) tile is evaluated once into
-// LDS in B-operand order, and the k range is split over the 8 waves
-// (split-K) with every operand of a wave's chunk loaded before its MFMAs;
-// partials are reduced in LDS in fixed wave order (deterministic).
+// cross_root_kernel: one workgroup per (16-row tile ti, group c of tile pairs,
+// output).  A pair is (p, T-1-p) of 16-column tiles of Q = K_x R; R upper
+// triangular means tile tj only needs k-blocks kb < 4(tj+1), so pairing the
+// shortest with the longest tile balances the MFMA count.  Group c holds
+// pairs CR_PAIRS c .. CR_PAIRS c + CR_PAIRS - 1: the training inputs are
+// staged in LDS and the K(x, X) tile is evaluated once into LDS in B-operand
+// order for the group's widest pair, then each pair's k range is split over
+// the 8 waves (split-K) with every operand of a wave's chunk loaded before its
+// MFMAs (the next pair's first batch is loaded while this pair's partials are
+// reduced); partials are reduced in LDS in fixed wave order (deterministic).
+// One pair per workgroup evaluates the kernel 6.25x over at n = 256 (the fill
+// is half of a workgroup's lifetime), but four pairs per workgroup made the
+// launch 11 us instead of 6 and lowered the forwards-in-flight throughput
+// (10.46 M against 11.01 M KG-evals/s, profiles/r02/r02za): with a few
+// forwards in flight the stage's latency, not its summed workgroup time,
+// sets the rate.  CR_PAIRS stays a tuning constant.
 constexpr int CR_WAVES = 8;
-constexpr int CR_U = 8;  // k-blocks per load batch
+constexpr int CR_U = 8;      // k-blocks per load batch
+constexpr int CR_PAIRS = 1;  // tile pairs per workgroup
+
+// LDS (doubles): the K tile [KB][64], the pair partials (their own region when
+// a workgroup reduces several pairs; else overlaying the K tile), the mean
+// partials, the staged inputs and alpha.  Pairs per workgroup: CR_PAIRS when
+// that fits the CU's 160 KiB, else 1 (large n with large d).
+__host__ __device__ inline size_t cross_lds_doubles(int np, int d, bool sep) {
+  const size_t kb = (size_t)(np / 4) * 64, pt = (size_t)CR_WAVES * 8 * 64;
+  return (sep ? kb + pt : (kb > pt ? kb : pt)) + CR_WAVES * 16 + (size_t)np * d + np;
+}
+__host__ __device__ inline int cross_pairs(int np, int d) {
+  return cross_lds_doubles(np, d, true) * sizeof(double) <= 160 * 1024 ? CR_PAIRS : 1;
+}
+__host__ __device__ inline int cross_groups(int np, int d) {
+  return ((np / 16 + 1) / 2 + cross_pairs(np, d) - 1) / cross_pairs(np, d);
+}
 
 // GRAD: the same contraction with the kernel replaced by its derivative in
 // the candidate's coordinate `gdim` (J = dK(x, X)/dx_g R, dmean = dK/dx_g alpha).
@@ -118,7 +142,7 @@ constexpr int CR_U = 8;  // k-blocks per load batch
 // kernel evaluations and the mean stay fp64.
 template <int DM, bool GRAD = false, class ET = double>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
-                                                ET* __restrict__ qout, double* __restrict__ mout, int ti, int p,
+                                                ET* __restrict__ qout, double* __restrict__ mout, int ti, int grp,
                                                 double* smem, unsigned long long* st = nullptr, int gdim = 0,
                                                 const double* __restrict__ qx_frag = nullptr,
                                                 double* __restrict__ qx_rm = nullptr,
@@ -131,36 +155,54 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   const int T = np / 16;
   const int KB = np / 4;
   const int P = (T + 1) / 2;
-  if (p >= P) return;
-  const int tA = p, tB = T - 1 - p;                  // tA <= tB
-  const int kbA = 4 * (tA + 1), kbB = 4 * (tB + 1);  // k-block extents (kbB >= kbA)
-  const int ncol = min(n, 4 * kbB);                  // training columns this pair needs
+  const int ppg = cross_pairs(np, d);
+  const int pb = grp * ppg, pe = min(P, pb + ppg);
+  if (pb >= pe) return;
+  const int kbW = 4 * (T - pb);           // k-block extent of the group's widest pair (its tile T-1-pb)
+  const int ncol = min(n, 4 * kbW);       // training columns the group needs
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  ET* kb_lds = reinterpret_cast<ET*>(smem);        // [KB][64]
-  double* part = smem;                           // [CR_WAVES][8][64], overlays kb_lds once the MFMAs are done
-  double* mred = smem + max(KB * 64, CR_WAVES * 8 * 64);  // [CR_WAVES][16]
-  double* xs = mred + CR_WAVES * 16;             // [np][d] staged training inputs
-  double* als = xs + (size_t)np * d;             // [np] alpha
+  ET* kb_lds = reinterpret_cast<ET*>(smem);     // [KB][64]
+  const bool sep = ppg > 1;
+  double* part = sep ? smem + KB * 64 : smem;   // [CR_WAVES][8][64] pair partials (cross_lds_doubles)
+  double* mred = smem + (sep ? KB * 64 + CR_WAVES * 8 * 64 : max(KB * 64, CR_WAVES * 8 * 64));  // [CR_WAVES][16]
+  double* xs = mred + CR_WAVES * 16;            // [np][d] staged training inputs
+  double* als = xs + (size_t)np * d;            // [np] alpha
 
-  // R fragments of this wave's first k-block batch: loaded before anything
-  // else so their latency overlaps the staging and the kernel evaluations.
+  // a pair's geometry for this wave: tiles, k-block extents, the wave's k chunk
   // (k-block ranges are even: kbA, kbB are multiples of 4 and chunk is even)
-  const int chunk = QW * ((kbB / QW + CR_WAVES - 1) / CR_WAVES);
-  const int k0 = wave * chunk;
-  const int k1 = min(kbB, k0 + chunk);
+  struct PairK {
+    int tA, tB, kbA, kbB, k0, k1;
+  };
+  auto pair_k = [&](int p) {
+    PairK q;
+    q.tA = p;
+    q.tB = T - 1 - p;  // tA <= tB
+    q.kbA = 4 * (q.tA + 1);
+    q.kbB = 4 * (q.tB + 1);
+    const int chunk = QW * ((q.kbB / QW + CR_WAVES - 1) / CR_WAVES);
+    q.k0 = wave * chunk;
+    q.k1 = min(q.kbB, q.k0 + chunk);
+    return q;
+  };
   ET ra[CR_U], rb[CR_U];
+  auto load_batch = [&](const PairK& q, int base) {
 #pragma unroll
-  for (int u = 0; u < CR_U; u += QW) {
-    const int j = min(k0 + u, kbB - QW) / QW;
-    frag_word<ET>(root, tB, j, lane, KB, rb + u);
-    frag_word<ET>(root, tA, min(j, kbA / QW - 1), lane, KB, ra + u);
-  }
+    for (int u = 0; u < CR_U; u += QW) {
+      const int j = min(base + u, q.kbB - QW) / QW;
+      frag_word<ET>(root, q.tB, j, lane, KB, rb + u);
+      frag_word<ET>(root, q.tA, min(j, q.kbA / QW - 1), lane, KB, ra + u);
+    }
+  };
+  // R fragments of this wave's first k-block batch of the first pair: loaded
+  // before anything else so their latency overlaps the staging and the fill.
+  PairK cur = pair_k(pb);
+  load_batch(cur, cur.k0);
 
   KST(st, 2);
-  const bool want_mean = (mout != nullptr) && (p == 0);  // p == 0 covers every column
+  const bool want_mean = (mout != nullptr) && (pb == 0);  // pair 0 covers every column
   // training inputs staged pre-scaled by 1/lengthscale (GPyTorch divides both
   // inputs by the lengthscale before the distance)
   for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e] * o.inv_lengthscale[e % d];
@@ -178,14 +220,14 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   __syncthreads();
 
   KST(st, 3);
-  // ---- fill K(x_row, X_col), col < 4*kbB, in B-operand order (zero outside)
+  // ---- fill K(x_row, X_col), col < 4*kbW, in B-operand order (zero outside)
   double mpart = 0.0;
   const double os = o.outputscale;
   const double ilg = GRAD ? o.inv_lengthscale[gdim] : 1.0;
   double xg = 0.0;  // the candidate's pre-scaled coordinate gdim (GRAD)
 #pragma unroll
   for (int k = 0; k < DM; ++k) xg = (k == gdim) ? xr[k] : xg;
-  const int fill = kbB * 64;
+  const int fill = kbW * 64;
   const int iters = (fill + CR_WAVES * WAVE - 1) / (CR_WAVES * WAVE);  // uniform trip count
   // one straight-line loop per covariance family (the switch stays outside)
   auto fill_loop = [&](auto kind_c) {
@@ -219,43 +261,6 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
     case DKG_RBF: fill_loop(std::integral_constant<int, DKG_RBF>{}); break;
     default: fill_loop(std::integral_constant<int, DKG_MATERN52>{}); break;
   }
-  __syncthreads();
-
-  KST(st, 4);
-  // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
-  typedef typename AccT<ET>::type acc_t;
-  acc_t accA2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  acc_t accB2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  const bool pairA = tA != tB;
-  for (int base = k0; base < k1; base += CR_U) {
-    ET bo[CR_U];
-    if (base != k0) {
-#pragma unroll
-      for (int u = 0; u < CR_U; u += QW) {
-        const int j = min(base + u, kbB - QW) / QW;
-        frag_word<ET>(root, tB, j, lane, KB, rb + u);
-        frag_word<ET>(root, tA, min(j, kbA / QW - 1), lane, KB, ra + u);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < CR_U; ++u) {
-      const int kb = min(base + u, kbB - 1);
-      bo[u] = (base + u < k1) ? kb_lds[kb * 64 + lane] : (ET)0;
-    }
-#pragma unroll
-    for (int u = 0; u < CR_U; ++u) {
-      accB2[u & 1] = mfma_t(rb[u], bo[u], accB2[u & 1]);
-      if (pairA && base + u < kbA) accA2[u & 1] = mfma_t(ra[u], bo[u], accA2[u & 1]);
-    }
-  }
-  const acc_t accA = accA2[0] + accA2[1];
-  const acc_t accB = accB2[0] + accB2[1];
-  __syncthreads();  // every wave is done with kb_lds before the partials overwrite it
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    part[(wave * 8 + r) * 64 + lane] = (double)accA[r];
-    part[(wave * 8 + 4 + r) * 64 + lane] = (double)accB[r];
-  }
   // mean partials: lanes l, l^16, l^32, l^48 share a row.
   if (want_mean) {
     mpart += partner_f64<4>(mpart);
@@ -264,16 +269,50 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   }
   __syncthreads();
 
-  KST(st, 5);
-  // ---- reduce partials in fixed wave order; wave w finalises (tile, reg) = w.
-  {
+  KST(st, 4);
+  typedef typename AccT<ET>::type acc_t;
+  for (int p = pb; p < pe; ++p) {
+    // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
+    acc_t accA2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    acc_t accB2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    const bool pairA = cur.tA != cur.tB;
+    for (int base = cur.k0; base < cur.k1; base += CR_U) {
+      ET bo[CR_U];
+      if (base != cur.k0) load_batch(cur, base);
+#pragma unroll
+      for (int u = 0; u < CR_U; ++u) {
+        const int kb = min(base + u, cur.kbB - 1);
+        bo[u] = (base + u < cur.k1) ? kb_lds[kb * 64 + lane] : (ET)0;
+      }
+#pragma unroll
+      for (int u = 0; u < CR_U; ++u) {
+        accB2[u & 1] = mfma_t(rb[u], bo[u], accB2[u & 1]);
+        if (pairA && base + u < cur.kbA) accA2[u & 1] = mfma_t(ra[u], bo[u], accA2[u & 1]);
+      }
+    }
+    const acc_t accA = accA2[0] + accA2[1];
+    const acc_t accB = accB2[0] + accB2[1];
+    const PairK done = cur;
+    if (p + 1 < pe) {  // the next pair's first batch, in flight during this pair's reduction
+      cur = pair_k(p + 1);
+      load_batch(cur, cur.k0);
+    }
+    __syncthreads();  // every wave is done with the previous pair's partials (and, overlaid, with kb_lds)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      part[(wave * 8 + r) * 64 + lane] = (double)accA[r];
+      part[(wave * 8 + 4 + r) * 64 + lane] = (double)accB[r];
+    }
+    __syncthreads();
+
+    // ---- reduce partials in fixed wave order; wave w finalises (tile, reg) = w.
     const int tsel = wave >> 2;  // 0 -> tA, 1 -> tB
     const int r = wave & 3;
     if (tsel == 1 || pairA) {
       double s = 0.0;
 #pragma unroll
       for (int w = 0; w < CR_WAVES; ++w) s += part[(w * 8 + tsel * 4 + r) * 64 + lane];
-      const int tj = tsel ? tB : tA;
+      const int tj = tsel ? done.tB : done.tA;
       // D = R^T K^T: lane holds Q[16ti + (l&15)][16tj + 4r + (l>>4)] = q_frag[ti][4tj + r][l]
       if constexpr (GRAD) {
         // J row-major [bpad][np] for the envelope's per-candidate row loads;
@@ -288,6 +327,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       }
     }
   }
+  KST(st, 5);
   if (want_mean && tid < 16) {
     double s = 0.0;
 #pragma unroll
@@ -348,9 +388,7 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_grad_plan_kernel(const 
                             blockIdx.y, smem, st, gdim, P->q[oi], gdim == 0 ? P->qxrm[oi] : nullptr);
 }
 
-size_t cross_root_lds_bytes(int np, int d) {
-  return ((size_t)std::max((np / 4) * 64, CR_WAVES * 8 * 64) + CR_WAVES * 16 + (size_t)np * d + np) * sizeof(double);
-}
+size_t cross_root_lds_bytes(int np, int d) { return cross_lds_doubles(np, d, cross_pairs(np, d) > 1) * sizeof(double); }
 
 // ---------------------------------------------------------------------------
 // posterior_cov_kernel: cov[b][k] = s k(x_b, D_k) - sum_l Q[b][l] Q_D[k][l]
@@ -656,7 +694,7 @@ hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s) {
 template <int DM>
 static hipError_t launch_cross_root_t(const CrossArgs& a, hipStream_t s) {
   const int np = pad16(a.o.n);
-  dim3 grid(pad16(a.rows) / 16, (np / 16 + 1) / 2, 1);
+  dim3 grid(pad16(a.rows) / 16, cross_groups(np, a.d), 1);
   const size_t lds = cross_root_lds_bytes(np, a.d);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)cross_root_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -677,7 +715,7 @@ template <int DM, class T>
 static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
                                       hipStream_t s, int stage) {
   if (stage == 0) {
-    dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m);
+    dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
     if (lds > 65536)
       (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel<DM, T>,
@@ -739,7 +777,7 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
 template <int DM>
 static hipError_t launch_cross_grad_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* dkg,
                                       hipStream_t s) {
-  dim3 grid(pad16(B) / 16, (h.max_np / 16 + 1) / 2, h.m * h.d);
+  dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m * h.d);
   const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)cross_grad_plan_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,

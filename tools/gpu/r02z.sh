@@ -1,7 +1,7 @@
 #!/bin/bash
-# psi by rational approximations (scalar-operand coefficients), envelope at 4 waves/SIMD (128 VGPRs)
+# psi by rational approximations, envelope at 4 waves/SIMD; cross stage with 4 tile pairs per workgroup
 set -uo pipefail
-out=gpurun_out/r02z
+out=gpurun_out/${OUT:-r02z}
 mkdir -p "$out"
 timeout -k 10 600 python3 -u -m pytest tests -x -q --timeout 200 --timeout-method thread -m gpu > "$out/tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 "$out/tests.log"; [ $rc -eq 0 ] || exit $rc

@@ -19,6 +19,9 @@
 using namespace dkg;
 
 constexpr int MAXL = 17, M = 2, MP = 2, NLINES = 1025, ITERS = 64;
+#ifndef CVSCALE
+#define CVSCALE 0.1  // slope scale: 0.1 gives a 47-entry list, 0.003 a short one (headline-like)
+#endif
 
 __device__ __forceinline__ double hash01(unsigned x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(512) void phase_kernel(double* out, unsigned long l
   for (int e = threadIdx.x; e < SL - STAGE_FRONT; e += blockDim.x) {
     const bool pad = e >= (NLINES - 1) * MP;
     lmu[e] = pad ? __builtin_nan("") : hash01(e * 2654435761u + blockIdx.x);
-    lcv[e] = pad ? __builtin_nan("") : 0.1 * hash01(e * 40503u + 17 + blockIdx.x);
+    lcv[e] = pad ? __builtin_nan("") : CVSCALE * hash01(e * 40503u + 17 + blockIdx.x);
   }
   __syncthreads();
   double* sb = lists + wave * 3 * ENV_CAP;
@@ -106,7 +109,8 @@ __global__ __launch_bounds__(512) void phase_kernel(double* out, unsigned long l
   build(la, lb);
   double acc = 0.0;
   int iacc = 0;
-  const FwdEnv f0 = env_extremes<MAXL>(la, lb);
+  FwdEnv f0 = env_extremes<MAXL>(la, lb);
+  env_ends<MAXL>(la, lb, f0);
   const EnvChords ch0 = env_chords(f0.bL, f0.aL, f0.bT, f0.aT, f0.bR, f0.aR);
   const int cnt0 = env_compact<MAXL, ENV_CAP>(la, lb, ch0, lane, sb, sa, si);
   __syncthreads();
