@@ -117,7 +117,10 @@ __device__ __forceinline__ void frag_word(const T* __restrict__ base, int tile, 
 // (10.46 M against 11.01 M KG-evals/s, profiles/r02/r02za): with a few
 // forwards in flight the stage's latency, not its summed workgroup time,
 // sets the rate.  CR_PAIRS stays a tuning constant.
-constexpr int CR_WAVES = 8;
+#ifndef DKG_CR_WAVES
+#define DKG_CR_WAVES 8
+#endif
+constexpr int CR_WAVES = DKG_CR_WAVES;
 constexpr int CR_U = 8;      // k-blocks per load batch
 constexpr int CR_PAIRS = 1;  // tile pairs per workgroup
 
@@ -305,10 +308,10 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
     }
     __syncthreads();
 
-    // ---- reduce partials in fixed wave order; wave w finalises (tile, reg) = w.
+    // ---- reduce partials in fixed wave order; wave w < 8 finalises (tile, reg) = w.
     const int tsel = wave >> 2;  // 0 -> tA, 1 -> tB
     const int r = wave & 3;
-    if (tsel == 1 || pairA) {
+    if (wave < 8 && (tsel == 1 || pairA)) {
       double s = 0.0;
 #pragma unroll
       for (int w = 0; w < CR_WAVES; ++w) s += part[(w * 8 + tsel * 4 + r) * 64 + lane];
@@ -393,17 +396,21 @@ size_t cross_root_lds_bytes(int np, int d) { return cross_lds_doubles(np, d, cro
 // ---------------------------------------------------------------------------
 // posterior_cov_kernel: cov[b][k] = s k(x_b, D_k) - sum_l Q[b][l] Q_D[k][l]
 // One workgroup (8 waves, 2 per SIMD) per 32 x 32 block = 2 x 2 output
-// tiles of one output; wave w computes tile (w % 4) over K-half (w / 4).
+// tiles of one output; wave w computes tile (w % 4) over K part (w / 4) of
+// PC_KS = 2.
 // Waves that share an operand tile and a K-half read it at the same time, so
 // a CU fetches each operand byte about once (L1); every load is a 16-byte
-// pair (two k-blocks).  K-halves meet in LDS; the K-half-0 wave evaluates
-// the kernel epilogue and stores.  Tiles with tk == 0 also produce the
-// candidates' own variances s - |Q_X[b]|^2.  At <= 128 VGPRs two blocks share
-// a CU: a 64 x 32 block of 16 waves (4 per SIMD) halves the workgroups but
-// holds the CU alone, and its forwards-in-flight throughput was lower
-// (profiles/r02/r02x).
+// pair (two k-blocks).  K parts meet in LDS in fixed order; the part-0
+// wave evaluates the kernel epilogue and stores.  Tiles with tk == 0 also produce the
+// candidates' own variances s - |Q_X[b]|^2.  At <= 128 VGPRs and 8 waves a
+// block shares its CU with another block or an envelope workgroup (also 8
+// waves at <= 128 VGPRs) of another forward in flight: 16 waves (K quarters,
+// 4 per SIMD) kept the block's lifetime and took the CU alone, and lowered
+// the forwards-in-flight throughput from 11.0 M to 9.0 M KG-evals/s
+// (profiles/r02/r02zc); a 64 x 32 block of 16 waves likewise (r02x).
 constexpr int PC_WAVES = 8;
 constexpr int PC_RB = 2;  // 16-row tiles per workgroup (32 candidates); 2 column tiles (32 lines)
+constexpr int PC_KS = PC_WAVES / (2 * PC_RB);  // K splits: the waves of one tile
 constexpr int PC_P = 8;  // 16-byte words per operand per load batch (16 k-blocks)
 
 // T = float (DKG_PLAN_F32): the contraction Q_X . Q_D in fp32 (quad-packed
@@ -416,8 +423,8 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   constexpr int QW = kpack<T>();
   typedef typename AccT<T>::type acc_t;
   constexpr int NT = 2 * PC_RB;  // output tiles per workgroup
-  __shared__ __attribute__((aligned(16))) double part[NT * 4 * 64];  // K-half 1 partial tiles
-  __shared__ double qpart[NT * 16];
+  __shared__ __attribute__((aligned(16))) double part[(PC_KS - 1) * NT * 4 * 64];  // K-split 1.. partial tiles
+  __shared__ double qpart[(PC_KS - 1) * NT * 16];
   unsigned long long* st = kst_slot(dst, P, 1);
   if (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1) return;  // ablation: empty covariance stage
   KST_BEGIN(st);
@@ -426,7 +433,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   const int N = P->N;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tt = wave % NT, half = wave / NT;
+  const int tt = wave % NT, ks = wave / NT;
   const int ti = PC_RB * blockIdx.y + (tt >> 1);
   const int tk = 2 * blockIdx.x + (tt & 1);
   const int KB = pad16(o.n) / 4;
@@ -434,9 +441,10 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   // tiles that exist in the workspace / state buffers (wave-uniform)
   const bool live = ti * 16 < pad16(B) && (tk * 16 < pad16(N) || (tk == 0 && !have_d));
   const bool want_var = tk == 0;
-  // K-half of this wave, in whole 16-byte words (QW k-blocks each)
+  // K part of this wave, in whole 16-byte words (QW k-blocks each)
   const int KP = KB / QW;
-  const int p0 = half * ((KP + 1) / 2), p1 = half ? KP : (KP + 1) / 2;
+  const int KPs = (KP + PC_KS - 1) / PC_KS;
+  const int p0 = min(KP, ks * KPs), p1 = min(KP, p0 + KPs);
   const T* qx;
   const T* qd;
   if constexpr (sizeof(T) == 8) {
@@ -467,7 +475,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   };
   if (live && p0 < p1) load_batch(p0);
   double r2[4] = {0.0, 0.0, 0.0, 0.0};
-  if (half == 0) {  // wave-uniform; P->disc is valid even when N == 0 (plan init)
+  if (ks == 0) {  // wave-uniform; P->disc is valid even when N == 0 (plan init)
     const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -499,17 +507,19 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     qsq += __shfl_xor(qsq, 16);
     qsq += __shfl_xor(qsq, 32);
   }
-  if (half == 1) {
+  if (ks > 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) part[(tt * 4 + r) * 64 + lane] = (double)accs[r];
-    if (want_var && lane < 16) qpart[tt * 16 + lane] = qsq;
+    for (int r = 0; r < 4; ++r) part[(((ks - 1) * NT + tt) * 4 + r) * 64 + lane] = (double)accs[r];
+    if (want_var && lane < 16) qpart[((ks - 1) * NT + tt) * 16 + lane] = qsq;
   }
   __syncthreads();
   KST(st, 4);
-  if (half == 0 && live) {
+  if (ks == 0 && live) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const double sum = (double)accs[r] + part[(tt * 4 + r) * 64 + lane];
+      double sum = (double)accs[r];
+#pragma unroll
+      for (int q = 0; q < PC_KS - 1; ++q) sum += part[((q * NT + tt) * 4 + r) * 64 + lane];  // fixed order
       const int b = ti * 16 + mfma_drow<T>(lane, r);
       if (b < B && k < N)  // line record k of candidate b, component oi (dkg_device.h cov_rec)
         P->cov_all[(size_t)b * P->cov_stride + (size_t)k * cov_rec(P->m) + oi] =
@@ -517,7 +527,10 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     }
     if (want_var && lane < 16) {
       const int bb = ti * 16 + lane;
-      if (bb < B) P->var[oi][bb] = o.outputscale - (qsq + qpart[tt * 16 + lane]);
+      double qs = qsq;
+#pragma unroll
+      for (int q = 0; q < PC_KS - 1; ++q) qs += qpart[(q * NT + tt) * 16 + lane];
+      if (bb < B) P->var[oi][bb] = o.outputscale - qs;
     }
   }
   KST_END(st);
