@@ -76,8 +76,9 @@ def parse():
     ap.add_argument("--profile-reps", type=int, default=50)
     ap.add_argument("--streams", type=int, default=4,
                     help="forward batches in flight: step k runs on stream k %% streams with its own plan workspace")
-    ap.add_argument("--graph", type=int, default=1,
-                    help="1 = replay each full exchange period (E forwards over the streams) as one captured HIP graph")
+    ap.add_argument("--graph", type=int, default=2,
+                    help="1 = replay each full exchange period (E forwards over the streams) as one captured HIP "
+                         "graph; 2 = one single-stream graph per stream per period, replayed side by side")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")
     ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
     ap.add_argument("--nd-steps", type=int, default=256,
@@ -197,7 +198,21 @@ class Throughput:
         xchg.flush(warmup)
         torch.cuda.synchronize()
         graphs = []
-        if graph and steps >= E:
+        if graph == 2 and steps >= E:
+            # per stream one single-stream graph of its rows r = i mod ns: replayed on its own stream, each
+            # enqueues its forwards as one batch (a graph forked over streams replays node by node)
+            for slot in range(2):
+                gs = []
+                for i in range(ns):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=streams[i] if i else torch.cuda.Stream(dev),
+                                          capture_error_mode="thread_local"):
+                        for r in range(i, E, ns):
+                            plans[i].forward_into(self.Xd, xchg.bufs[slot][r])
+                    gs.append(g)
+                graphs.append(gs)
+            torch.cuda.synchronize()
+        elif graph and steps >= E:
             # one graph per exchange buffer: the E forwards of a period, forked over the streams exactly
             # as the eager path does; replayed on the main stream, so the collective after it orders as before
             for slot in range(2):
@@ -224,19 +239,34 @@ class Throughput:
         for s in streams[1:]:
             s.wait_stream(main_s)
         k0 = 0
+        host = 0.0  # host seconds inside the launch calls (replay / plan.forward_into)
         if graphs:
             while k0 + E <= steps:
                 xchg.row(k0)
-                graphs[(k0 // E) % 2].replay()
+                th = time.perf_counter()
+                g = graphs[(k0 // E) % 2]
+                if graph == 2:
+                    for s in streams[1:]:
+                        s.wait_stream(main_s)
+                    for i in range(ns):
+                        with torch.cuda.stream(streams[i]):
+                            g[i].replay()
+                    join()
+                else:
+                    g.replay()
+                host += time.perf_counter() - th
                 xchg.done(k0 + E - 1)
                 k0 += E
         for k in range(k0, steps):
+            th = time.perf_counter()
             step(k)
+            host += time.perf_counter() - th
         join()
         xchg.flush(steps)
         ev1.record()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
+        self.host_us_per_step = host / max(1, steps) * 1e6
         if world > 1:
             dist.barrier()
         gpu_s = ev0.elapsed_time(ev1) / 1e3
@@ -343,7 +373,7 @@ def main():
     if args.streams > 1 or args.graph:
         e1 = tp.run(1, args.steps, args.warmup, False, world)
         single = {"value": world * w.B * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
-    elapsed = tp.run(max(1, args.streams), args.steps, args.warmup, bool(args.graph), world)
+    elapsed = tp.run(max(1, args.streams), args.steps, args.warmup, args.graph, world)
     value = world * w.B * args.steps / elapsed
 
     # ---- per-kernel rooflines; the dominant kernel's is the line's `roofline`
@@ -406,7 +436,7 @@ def main():
     nd = None
     if args.nd_steps > 0 and args.workload == "headline" and args.precision == "fp64":
         wn, _, Dn, _, _, _, tpn = setup("headline_nd")
-        en = tpn.run(max(1, args.streams), args.nd_steps, min(args.warmup, 10), bool(args.graph), world)
+        en = tpn.run(max(1, args.streams), args.nd_steps, min(args.warmup, 10), args.graph, world)
         env_us = tpn.plan.time_stage(tpn.Xd, 2, args.profile_reps) * 1e3
         nd = {"workload": "headline_nd", "value": world * wn.B * args.nd_steps / en, "unit": "KG-evals/s",
               "steps": args.nd_steps, "ms_per_step": en / args.nd_steps * 1e3, "envelope_us": env_us,
@@ -442,7 +472,9 @@ def main():
                                       f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'} "
                                       f"per {E} forward batches",
                        "exchange_every": E, "streams": max(1, args.streams),
-                       "hip_graph": bool(args.graph)},
+                       "hip_graph": {0: "off", 1: "one graph forked over the streams",
+                                     2: "one single-stream graph per stream"}.get(args.graph, str(args.graph))},
+            "host_launch_us_per_step": tp.host_us_per_step,
             "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
