@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   const bool full = target < 0;
   static_assert(STREAM || MAXL == 2 || MAXL == 8 || MAXL == 17 || MAXL == 33, "slot bucket");
   unsigned long long* st = kst_slot(dst, P, 2);
-  if (__builtin_amdgcn_readfirstlane(P->debug_env) & 2) return;  // ablation: empty envelope stage
+  if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
   KST_BEGIN(st);
 
   // The DMA sources first, in one scalar-load batch: the LDS-DMA intrinsics

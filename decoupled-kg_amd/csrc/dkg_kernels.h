@@ -12,6 +12,13 @@ namespace dkg {
 // per-output 8-byte reads the compiler pairs into ds_read2st64_b64 (128 B/clk).
 __host__ __device__ constexpr int cov_rec(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 4 ? 4 : 8; }
 
+// Stage ablations (empty cross / covariance / envelope launches selected by
+// DKG_DEBUG_COV_FLAGS 2 / 1 and DKG_DEBUG_ENV_FLAGS 2) exist only in builds
+// with -DDKG_ABLATIONS=1: the check is a dependent scalar load at kernel entry.
+#ifndef DKG_ABLATIONS
+#define DKG_ABLATIONS 0
+#endif
+
 // Everything a forward needs besides the candidates, resident in device memory
 // (written once per (model, discretisation, weights) by dkg_plan_init): the
 // kernels take a pointer to it, so each launch carries ~40 bytes of arguments
@@ -21,7 +28,7 @@ struct Plan {
   int32_t m, d, N, S, target;       // target < 0: all outputs observed
   int32_t max_B, max_np;            // workspace sized for max_B candidates; max n_pad over outputs
   int32_t sw, split;                // envelope geometry: waves per workgroup, workgroups per candidate
-  int32_t debug_env, debug_cov;     // ablation switches (0 in production; DESIGN.md "Ablations")
+  int32_t debug_env, debug_cov;     // test / ablation switches (0 in production)
   int32_t debug_stamp;              // 1: per-workgroup phase stamps into g_kstamps (0 in production)
   int32_t grad;                     // workspace holds the gradient buffers (DKG_PLAN_GRAD)
   int32_t bpad;                     // pad16(max_B): rows of the fragment-packed candidate buffers

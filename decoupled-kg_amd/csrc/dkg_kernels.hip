@@ -363,7 +363,7 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
       P->tickets[i] = 0;
     }
   }
-  if (__builtin_amdgcn_readfirstlane(P->debug_cov) & 2) return;  // ablation: empty cross stage
+  if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 2)) return;  // ablation: empty cross stage
   if constexpr (sizeof(T) == 8) {
     cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
   } else {
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   __shared__ __attribute__((aligned(16))) double part[(PC_KS - 1) * NT * 4 * 64];  // K-split 1.. partial tiles
   __shared__ double qpart[(PC_KS - 1) * NT * 16];
   unsigned long long* st = kst_slot(dst, P, 1);
-  if (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1) return;  // ablation: empty covariance stage
+  if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1)) return;  // ablation: empty covariance stage
   KST_BEGIN(st);
   const int oi = blockIdx.z;
   const dkg_output& o = P->o[oi];
