@@ -265,8 +265,10 @@ __device__ __forceinline__ EdgeSum walk_table(int nc, int lane, const double* sb
   constexpr int CH = JL < 4 ? JL : 4;
   double xb = INFINITY, bb = INFINITY, ab = -INFINITY;
   int kb = KEY_NONE, jb = -1;
+  // only the chunks that hold list entries (a 17-entry list in the 32-row table: 3 of 4 chunks)
+  const int jl = min(JL, (nc + G - 1) / G);
 #pragma unroll 1
-  for (int q0 = 0; q0 < JL; q0 += CH) {
+  for (int q0 = 0; q0 < jl; q0 += CH) {
     double ebj[CH], eaj[CH];
     int ekj[CH];
 #pragma unroll
