@@ -474,13 +474,17 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     }
   };
   if (live && p0 < p1) load_batch(p0);
-  double r2[4] = {0.0, 0.0, 0.0, 0.0};
+  // the epilogue's kernel terms s k(x_b, D_k), evaluated before the contraction: their VALU work
+  // overlaps the other waves' MFMAs instead of trailing the block
+  double kv[4] = {0.0, 0.0, 0.0, 0.0};
   if (ks == 0) {  // wave-uniform; P->disc is valid even when N == 0 (plan init)
     const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
+    const double os = o.outputscale;
+    const int kind = o.kernel;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = ti * 16 + mfma_drow<T>(lane, r);
-      r2[r] = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d);
+      kv[r] = os * kernel_profile(kind, scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d));
     }
   }
   KST(st, 2);
@@ -522,8 +526,7 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
       for (int q = 0; q < PC_KS - 1; ++q) sum += part[((q * NT + tt) * 4 + r) * 64 + lane];  // fixed order
       const int b = ti * 16 + mfma_drow<T>(lane, r);
       if (b < B && k < N)  // line record k of candidate b, component oi (dkg_device.h cov_rec)
-        P->cov_all[(size_t)b * P->cov_stride + (size_t)k * cov_rec(P->m) + oi] =
-            o.outputscale * kernel_profile(o.kernel, r2[r]) - sum;
+        P->cov_all[(size_t)b * P->cov_stride + (size_t)k * cov_rec(P->m) + oi] = kv[r] - sum;
     }
     if (want_var && lane < 16) {
       const int bb = ti * 16 + lane;
