@@ -44,10 +44,11 @@ def test_stage_model_matches_design_table():
 
 
 def test_default_run_is_whole_graph_periods(monkeypatch):
-    """The default bench line: four forward batches in flight, graph replay on, and a step count that is
-    a whole number of exchange periods, so no timed step falls back to eager launches."""
+    """The default bench line: four forward batches in flight, one single-stream graph per stream
+    replayed (graph mode 2), and a step count that is a whole number of exchange periods, so no timed
+    step falls back to eager launches."""
     b = _bench()
     monkeypatch.setattr("sys.argv", ["bench.py"])
     a = b.parse()
-    assert a.gpus == 1 and a.streams == 4 and a.graph == 1
+    assert a.gpus == 1 and a.streams == 4 and a.graph == 2
     assert a.steps % a.exchange_every == 0
