@@ -57,33 +57,113 @@ __device__ __forceinline__ float4 frag_quad(const float* __restrict__ base, int 
   return reinterpret_cast<const float4*>(base)[((size_t)tile * (KB >> 2) + j) * 64 + lane];
 }
 
+// psi's coefficients in one constant table (offsets PSI_OFF_*): exp's Taylor
+// terms 1/k! (k = 0..13), then PA, QA (x < 4) and PB, QB (x >= 4) from
+// tools/fit_psi.py.
+static __constant__ double PSI_TAB[46] = {
+    // EXP_TAYLOR
+    1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664, 0.008333333333333333, 0.001388888888888889, 0.0001984126984126984, 2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07, 2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10,
+    // PSI_PA
+    1.0, 2.796346091120482, 4.476998603222499, 4.347508891535361, 2.7165796377890157, 1.0037192400095971, 0.17325326370833247, -4.618396778934904e-05, 3.3360288569271207e-06,
+    // PSI_QA
+    1.0, 7.809602640382476, 27.628540187254945, 58.0088790797422, 79.3523289449324, 72.75170128287581, 43.91331216452371, 16.08152617590387, 2.7670522859865594,
+    // PSI_PB
+    0.9981308338834465, 3.6598787850514367, 4.641485909810474, 2.472764850018868, 0.5303020141112789, 0.034608494860324725, 0.00012399724831674248,
+    // PSI_QB
+    1.0, 3.8515503731650442, 5.30522462058383, 3.263540634985728, 0.913625609211908, 0.10482146071245484, 0.003532980749196329,
+};
+constexpr int PSI_OFF_EXP = 0;
+constexpr int PSI_OFF_PA = 14;
+constexpr int PSI_OFF_QA = 23;
+constexpr int PSI_OFF_PB = 32;
+constexpr int PSI_OFF_QB = 39;
+
+// a * b + c with c an SGPR operand: one v_fma_f64.  Written out because the
+// compiler otherwise picks v_fmac_f64 (addend tied to the destination) and
+// copies every scalar coefficient into VGPRs first, two v_mov per FMA.
+__device__ __forceinline__ double fma_scalar_addend(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+
+// Horner over N coefficients at c (c[0] the constant term), c in SGPRs.
+template <int N, class Ptr>
+__device__ __forceinline__ double horner(Ptr c, double v) {
+  double r = fma_scalar_addend(c[N - 1], v, c[N - 2]);
+#pragma unroll
+  for (int i = N - 3; i >= 0; --i) r = fma_scalar_addend(r, v, c[i]);
+  return r;
+}
+
+// The table through an opaque constant-address-space pointer: the
+// coefficients are scalar loads (s_load, the scalar cache) at the use, SGPR
+// operands of the FMAs, never constants the compiler materialises early in
+// VGPRs (a generic pointer here compiled to per-lane flat loads).
+typedef const __attribute__((address_space(4))) double* const_dptr;
+__device__ __forceinline__ const_dptr psi_tab() {
+  const_dptr c = (const_dptr)PSI_TAB;
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
+// exp(y) for y <= 0 (0 below -760, where it underflows, branch-free): y = k ln2 + r with
+// the reduction in two FMAs (ln2 to 2^-106), the Taylor polynomial (terms to
+// k = 13: truncation ~4e-18 on |r| <= ln2 / 2) from the table, v_ldexp
+// (gradual underflow).  Relative error ~1e-16.
+__device__ __forceinline__ double exp_nonpos(double y, const_dptr tab) {
+  y = (y < -760.0) ? -760.0 : y;  // 2^k underflows ldexp to 0; NaN passes
+  const double k = rint(y * 1.4426950408889634);
+  double r = fma(-k, 0.6931471805599453, y);
+  r = fma(-k, 2.3190468138462996e-17, r);
+  return ldexp(horner<14>(tab + PSI_OFF_EXP, r), (int)k);
+}
+
+// sqrt for x >= 0 (no denormal inputs; 0 -> 0): v_rsq_f64 and two
+// Goldschmidt steps, ~1 ulp; libm's sqrt adds denormal scaling and special
+// cases the kernel profiles never need.
+__device__ __forceinline__ double sqrt_nonneg(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-g, h, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  const double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return (x > 0.0) ? g : 0.0;
+}
+
 // Kernel profile of ScaleKernel(base) at squared scaled distance r2:
 // gpytorch MaternKernel.forward / RBFKernel (factory.py:116 catalog).
-__device__ __forceinline__ double kernel_profile(int kind, double r2) {
-  if (kind == DKG_RBF) return exp(-0.5 * r2);
-  const double r = sqrt(r2);
-  if (kind == DKG_MATERN12) return exp(-r);
+// exp and sqrt as exp_nonpos / sqrt_nonneg (arguments are <= 0 / >= 0 here):
+// about half the instructions of libm's, whose range and special-case
+// handling these arguments never need (~1 ulp either way).
+__device__ __forceinline__ double kernel_profile(int kind, double r2, const_dptr tab = psi_tab()) {
+  if (kind == DKG_RBF) return exp_nonpos(-0.5 * r2, tab);
+  const double r = sqrt_nonneg(r2);
+  if (kind == DKG_MATERN12) return exp_nonpos(-r, tab);
   if (kind == DKG_MATERN32) {
     const double t = 1.7320508075688772 * r;
-    return (t + 1.0) * exp(-t);
+    return (t + 1.0) * exp_nonpos(-t, tab);
   }
   const double t = 2.23606797749979 * r;  // sqrt(5) r
-  return (t + 1.0 + (5.0 / 3.0) * r2) * exp(-t);
+  return (t + 1.0 + (5.0 / 3.0) * r2) * exp_nonpos(-t, tab);
 }
 
 // Same with the family fixed at compile time (branch-free in unrolled loops).
+// Loops pass the table pointer from outside (one address computation).
 template <int KIND>
-__device__ __forceinline__ double kernel_profile_t(double r2) {
+__device__ __forceinline__ double kernel_profile_t(double r2, const_dptr tab = psi_tab()) {
   if constexpr (KIND == DKG_RBF) {
-    return exp(-0.5 * r2);
+    return exp_nonpos(-0.5 * r2, tab);
   } else if constexpr (KIND == DKG_MATERN12) {
-    return exp(-sqrt(r2));
+    return exp_nonpos(-sqrt_nonneg(r2), tab);
   } else if constexpr (KIND == DKG_MATERN32) {
-    const double t = 1.7320508075688772 * sqrt(r2);
-    return (t + 1.0) * exp(-t);
+    const double t = 1.7320508075688772 * sqrt_nonneg(r2);
+    return (t + 1.0) * exp_nonpos(-t, tab);
   } else {
-    const double t = 2.23606797749979 * sqrt(r2);
-    return (t + 1.0 + (5.0 / 3.0) * r2) * exp(-t);
+    const double t = 2.23606797749979 * sqrt_nonneg(r2);
+    return (t + 1.0 + (5.0 / 3.0) * r2) * exp_nonpos(-t, tab);
   }
 }
 
@@ -294,59 +374,8 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 // from constant memory through an opaque pointer (horner), one scalar operand
 // per FMA.
 
-// psi's coefficients in one constant table (offsets PSI_OFF_*): exp's Taylor
-// terms 1/k! (k = 0..13), then PA, QA (x < 4) and PB, QB (x >= 4) from
-// tools/fit_psi.py.
-static __constant__ double PSI_TAB[46] = {
-    // EXP_TAYLOR
-    1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664, 0.008333333333333333, 0.001388888888888889, 0.0001984126984126984, 2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07, 2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10,
-    // PSI_PA
-    1.0, 2.796346091120482, 4.476998603222499, 4.347508891535361, 2.7165796377890157, 1.0037192400095971, 0.17325326370833247, -4.618396778934904e-05, 3.3360288569271207e-06,
-    // PSI_QA
-    1.0, 7.809602640382476, 27.628540187254945, 58.0088790797422, 79.3523289449324, 72.75170128287581, 43.91331216452371, 16.08152617590387, 2.7670522859865594,
-    // PSI_PB
-    0.9981308338834465, 3.6598787850514367, 4.641485909810474, 2.472764850018868, 0.5303020141112789, 0.034608494860324725, 0.00012399724831674248,
-    // PSI_QB
-    1.0, 3.8515503731650442, 5.30522462058383, 3.263540634985728, 0.913625609211908, 0.10482146071245484, 0.003532980749196329,
-};
-constexpr int PSI_OFF_EXP = 0;
-constexpr int PSI_OFF_PA = 14;
-constexpr int PSI_OFF_QA = 23;
-constexpr int PSI_OFF_PB = 32;
-constexpr int PSI_OFF_QB = 39;
-
-// Horner over N coefficients at c (c[0] the constant term).
-template <int N>
-__device__ __forceinline__ double horner(const double* c, double v) {
-  double r = c[N - 1];
-#pragma unroll
-  for (int i = N - 2; i >= 0; --i) r = fma(r, v, c[i]);
-  return r;
-}
-
-// The table through an opaque pointer: the coefficients are scalar loads at
-// the use (SGPR operands of the FMAs), never constants the compiler
-// materialises early in VGPRs.
-__device__ __forceinline__ const double* psi_tab() {
-  const double* c = PSI_TAB;
-  asm volatile("" : "+s"(c));
-  return c;
-}
-
-// exp(y) for y <= 0 (0 below -760, where it underflows): y = k ln2 + r with
-// the reduction in two FMAs (ln2 to 2^-106), the Taylor polynomial (terms to
-// k = 13: truncation ~4e-18 on |r| <= ln2 / 2) from the table, v_ldexp
-// (gradual underflow).  Relative error ~1e-16.
-__device__ __forceinline__ double exp_nonpos(double y, const double* tab) {
-  if (!(y > -760.0)) return (y != y) ? y : 0.0;
-  const double k = rint(y * 1.4426950408889634);
-  double r = fma(-k, 0.6931471805599453, y);
-  r = fma(-k, 2.3190468138462996e-17, r);
-  return ldexp(horner<14>(tab + PSI_OFF_EXP, r), (int)k);
-}
-
 __device__ __forceinline__ double psi(double c) {
-  const double* tab = psi_tab();
+  const const_dptr tab = psi_tab();
   const double x = fabs(c);
   const double x2 = x * x, x2l = fma(x, x, -x2);  // x^2 = x2 + x2l exactly
   const double e = 0.3989422804014327 * exp_nonpos(-0.5 * x2, tab) * fma(-0.5, x2l, 1.0);

@@ -235,6 +235,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   // one straight-line loop per covariance family (the switch stays outside)
   auto fill_loop = [&](auto kind_c) {
     constexpr int KIND = decltype(kind_c)::value;
+    const const_dptr tab = psi_tab();
 #pragma unroll 4
     for (int it = 0; it < iters; ++it) {
       const int e = tid + it * CR_WAVES * WAVE;
@@ -250,7 +251,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       if constexpr (GRAD) {
         kv = os * kernel_dprofile_t<KIND>(r2) * (xg - xs[(size_t)cc * d + gdim]) * ilg;
       } else {
-        kv = os * kernel_profile_t<KIND>(r2);
+        kv = os * kernel_profile_t<KIND>(r2, tab);
       }
       const double v = (rv && col < n) ? kv : 0.0;
       const double al = als[cc];  // staged only when want_mean; otherwise ignored
@@ -481,10 +482,11 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
     const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
     const double os = o.outputscale;
     const int kind = o.kernel;
+    const const_dptr tab = psi_tab();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = ti * 16 + mfma_drow<T>(lane, r);
-      kv[r] = os * kernel_profile(kind, scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d));
+      kv[r] = os * kernel_profile(kind, scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d), tab);
     }
   }
   KST(st, 2);
