@@ -474,19 +474,49 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
       frag_word<T>(dsrc, dt, j, lane, KB, vd[u]);
     }
   };
+  // The epilogue's kernel terms s k(x_b, D_k), evaluated by the K-part-0 waves before the
+  // contraction: their VALU work overlaps the K-part-1 waves' MFMAs on the same SIMDs (splitting
+  // the terms over both parts overlapped nothing and lengthened the block: profiles/r02/r02zm).
+  // At small d (EPI_FIRST) their inputs are loaded ahead of the first operand batch: loads
+  // complete in order, so the terms' wait does not include the batch and their VALU work overlaps
+  // its round trip.  At larger d the inputs would stay live beside the batch (over 128 VGPRs).
+  constexpr bool EPI_FIRST = DM <= 2;
+  constexpr int RV = 4;
+  const bool epi = ks == 0;  // wave-uniform
+  // line k's coordinates (P->disc is valid even when N == 0: plan init)
+  auto disc_row = [&]() { return P->disc + (size_t)min(k, max(N, 1) - 1) * d; };
+  double ek[EPI_FIRST ? DM : 1], eb[RV][EPI_FIRST ? DM : 1];
+  if (EPI_FIRST && epi) {
+    const double* xk = disc_row();
+#pragma unroll
+    for (int c = 0; c < DM; ++c) {
+      ek[c] = xk[min(c, d - 1)];
+#pragma unroll
+      for (int rr = 0; rr < RV; ++rr)
+        eb[rr][c] = xnew[(size_t)min(ti * 16 + mfma_drow<T>(lane, rr), B - 1) * d + min(c, d - 1)];
+    }
+  }
   if (live && p0 < p1) load_batch(p0);
-  // the epilogue's kernel terms s k(x_b, D_k), evaluated before the contraction: their VALU work
-  // overlaps the other waves' MFMAs instead of trailing the block
-  double kv[4] = {0.0, 0.0, 0.0, 0.0};
-  if (ks == 0) {  // wave-uniform; P->disc is valid even when N == 0 (plan init)
-    const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
+  double kv[RV] = {};
+  if (epi) {
     const double os = o.outputscale;
     const int kind = o.kernel;
     const const_dptr tab = psi_tab();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = ti * 16 + mfma_drow<T>(lane, r);
-      kv[r] = os * kernel_profile(kind, scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d), tab);
+    for (int rr = 0; rr < RV; ++rr) {
+      double r2;
+      if constexpr (EPI_FIRST) {
+        r2 = 0.0;  // scaled_r2_dm's arithmetic on the preloaded inputs
+#pragma unroll
+        for (int c = 0; c < DM; ++c) {
+          const double t = (eb[rr][c] - ek[c]) * o.inv_lengthscale[min(c, d - 1)];
+          r2 = fma(t, (c < d) ? t : 0.0, r2);
+        }
+      } else {
+        const int b = ti * 16 + mfma_drow<T>(lane, rr);
+        r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, disc_row(), o.inv_lengthscale, d);
+      }
+      kv[rr] = os * kernel_profile(kind, r2, EPI_FIRST ? tab : psi_tab());
     }
   }
   KST(st, 2);
