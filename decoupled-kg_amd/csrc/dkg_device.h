@@ -273,6 +273,40 @@ __device__ __forceinline__ FwdEnv env_extremes(const double (&la)[MAXL], const d
   return f;
 }
 
+// The flat-first order (envelope forward): T's intercept and slope alone, then
+// the flat test; the slope range and the short-circuit test (env_span) only for
+// the pairs it does not settle.  A flat pair's KG is 0 whichever test decides it.
+template <int MAXL>
+__device__ __forceinline__ void env_top(const double (&la)[MAXL], const double (&lb)[MAXL], FwdEnv& f) {
+  double amax = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) amax = fmax_raw(amax, la[t]);
+  DKG_BUTTERFLY_ROW({ amax = fmax_raw(amax, partner_f64<S_>(amax)); })
+  f.aT = combine_rows(amax, [](double a, double b) { return fmax(a, b); });
+  f.bT = tie_fold<MAXL, false>(la, f.aT, lb);
+  f.aL = f.aR = -INFINITY;
+  f.cnt = 0;
+  f.status = 0;
+}
+
+// env_extremes' slope range and status after env_top.
+template <int MAXL>
+__device__ __forceinline__ void env_span(const double (&lb)[MAXL], FwdEnv& f) {
+  double bmin = INFINITY, bmax = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXL; ++t) {
+    bmin = fmin_raw(bmin, lb[t]);
+    bmax = fmax_raw(bmax, lb[t]);
+  }
+  DKG_BUTTERFLY_ROW({
+    bmin = fmin_raw(bmin, partner_f64<S_>(bmin));
+    bmax = fmax_raw(bmax, partner_f64<S_>(bmax));
+  })
+  f.bL = combine_rows(bmin, [](double a, double b) { return fmin(a, b); });
+  f.bR = combine_rows(bmax, [](double a, double b) { return fmax(a, b); });
+  f.status = uniform(fmax(fabs(f.bL), fabs(f.bR)) >= 1e-9 && f.bL < f.bR) ? 0 : 1;
+}
+
 // Flat envelope: line T (max a, then min b) lies strictly above every other
 // line, exact copies of T aside, on the whole of [-ENV_FLAT_Z, ENV_FLAT_Z].
 // Then every envelope breakpoint has |c| > ENV_FLAT_Z > 40, every edge term
@@ -356,23 +390,29 @@ __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, in
     double la[MAXL], lb[MAXL];
     build(la, lb);
     if (pst) pst[1] = __builtin_amdgcn_s_memtime();
-    f = env_extremes<MAXL>(la, lb);
-    if (pst) pst[2] = __builtin_amdgcn_s_memtime();
+    if (flat_ok) {
+      env_top<MAXL>(la, lb, f);
+      if (pst) pst[2] = __builtin_amdgcn_s_memtime();
+      if (env_flat<MAXL>(la, lb, f)) {
+        *nhull = 0;  // not walked: KG_w = 0 exactly (env_flat)
+        if (pst) {
+          pst[3] = __builtin_amdgcn_s_memtime();
+          pst[6] = 0;
+          pst[7] = 1ull << 34;
+        }
+        return EdgeSum{0.0, 0.0, 0.0, false};
+      }
+      env_span<MAXL>(lb, f);
+    } else {
+      f = env_extremes<MAXL>(la, lb);
+      if (pst) pst[2] = __builtin_amdgcn_s_memtime();
+    }
     if (f.status == 1) {
       if (out && out->cap > 0) {
         const int k = first_max_index<MAXL>(la, nl, lane, f.aT);
         if (lane == 0) out->idx[0] = k;
       }
       *nhull = 1;
-      return EdgeSum{0.0, 0.0, 0.0, false};
-    }
-    if (flat_ok && env_flat<MAXL>(la, lb, f)) {
-      *nhull = 0;  // not walked: KG_w = 0 exactly (env_flat)
-      if (pst) {
-        pst[3] = __builtin_amdgcn_s_memtime();
-        pst[6] = 0;
-        pst[7] = 1ull << 34;
-      }
       return EdgeSum{0.0, 0.0, 0.0, false};
     }
     env_ends<MAXL>(la, lb, f);
@@ -1729,7 +1769,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
       }
     }
   }
-  __syncthreads();
+  if (st) __syncthreads();  // workgroup-uniform: the end stamp covers every wave
   KST_END(st);
 }
 
