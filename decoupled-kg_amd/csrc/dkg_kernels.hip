@@ -143,11 +143,12 @@ __host__ __device__ inline int cross_groups(int np, int d) {
 // the candidate's coordinate `gdim` (J = dK(x, X)/dx_g R, dmean = dK/dx_g alpha).
 // T = float (DKG_PLAN_F32): R^T and Q in fp32 (quad-packed), fp32 MFMA; the
 // kernel evaluations and the mean stay fp64.
+// qx_rm (fp64 forward only): also write Q row-major [rows_pad][n_pad] (the gradient envelope's rows).
 template <int DM, bool GRAD = false, class ET = double>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
                                                 ET* __restrict__ qout, double* __restrict__ mout, int ti, int grp,
                                                 double* smem, unsigned long long* st = nullptr, int gdim = 0,
-                                                const double* __restrict__ qx_frag = nullptr,
+                                                const double* __restrict__ /*unused*/ = nullptr,
                                                 double* __restrict__ qx_rm = nullptr,
                                                 const ET* __restrict__ root = nullptr) {
   static_assert(!GRAD || sizeof(ET) == 8, "the gradient stage is fp64");
@@ -323,11 +324,12 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
         // the gdim == 0 workgroups also copy Q_X's matching entries row-major
         const size_t rm = (size_t)(16 * ti + (lane & 15)) * np + 16 * tj + 4 * r + (lane >> 4);
         qout[rm] = s;
-        if (qx_rm) qx_rm[rm] = qx_frag[frag_index(ti, 4 * tj + r, lane, KB)];
       } else {
         // D row dr = column 16 tj + dr of Q: k-block 4 tj + dr/4, operand lane (l & 15) | (dr % 4) << 4
         const int dr = mfma_drow<ET>(lane, r);
         qout[fragT_index<ET>(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = (ET)s;
+        if constexpr (sizeof(ET) == 8)
+          if (qx_rm) qx_rm[(size_t)(16 * ti + (lane & 15)) * np + 16 * tj + dr] = s;
       }
     }
   }
@@ -373,23 +375,38 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
   }
 }
 
-// Gradient cross stage: grid (B tiles, pairs, outputs x d); z = oi * d + g
-// writes J_g = dK(x, X)/dx_g R (fragment-packed) and dmean/dx_g for output oi.
-// Workgroup (0,0,0) clears the gradient accumulator dkg[B x d].
+// Value + gradient cross stage, one launch: grid (B tiles, pairs, m + m d).
+// z < m: the forward cross stage of output z (Q_X fragment-packed and row-major, means; kg and the
+// tickets cleared).  z >= m, z - m = oi d + g: J_g = dK(x, X)/dx_g R (row-major) and dmean/dx_g for
+// output oi; the first of these workgroups clears the gradient accumulator dkg[B x d].  The two halves
+// read only x and the state, so they run side by side in one launch (at B = 1 the value+gradient chain
+// is latency-bound: one launch and one dependency gap fewer than two cross launches).
 template <int DM>
-__global__ __launch_bounds__(CR_WAVES * WAVE) void cross_grad_plan_kernel(const Plan* __restrict__ P,
-                                                                          const double* __restrict__ xnew, int B,
-                                                                          double* __restrict__ dkg, int dst) {
+__global__ __launch_bounds__(CR_WAVES * WAVE) void cross_fwd_grad_kernel(const Plan* __restrict__ P,
+                                                                         const double* __restrict__ xnew, int B,
+                                                                         double* __restrict__ kg,
+                                                                         double* __restrict__ dkg, int dst) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   unsigned long long* st = kst_slot(dst, P, 0);
-  const int d = P->d;
-  const int oi = blockIdx.z / d, gdim = blockIdx.z % d;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+  const int m = P->m, d = P->d;
+  const int z = blockIdx.z;
+  if (z < m) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && z == 0)
+      for (int i = threadIdx.x; i < B; i += blockDim.x) {
+        kg[i] = 0.0;
+        P->tickets[i] = 0;
+      }
+    cross_root_impl<DM>(P->o[z], d, xnew, B, P->q[z], P->mux[z], blockIdx.x, blockIdx.y, smem, st, 0, nullptr,
+                        P->qxrm[z]);
+    return;
+  }
+  const int oi = (z - m) / d, gdim = (z - m) % d;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && z == m)
     for (int i = threadIdx.x; i < B * d; i += blockDim.x) dkg[i] = 0.0;
   const dkg_output& o = P->o[oi];
   const size_t mat = (size_t)P->bpad * pad16(o.n);
   cross_root_impl<DM, true>(o, d, xnew, B, P->jq[oi] + gdim * mat, P->gmu[oi] + (size_t)gdim * P->bpad, blockIdx.x,
-                            blockIdx.y, smem, st, gdim, P->q[oi], gdim == 0 ? P->qxrm[oi] : nullptr);
+                            blockIdx.y, smem, st, gdim);
 }
 
 size_t cross_root_lds_bytes(int np, int d) { return cross_lds_doubles(np, d, cross_pairs(np, d) > 1) * sizeof(double); }
@@ -823,29 +840,29 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
 }
 
 template <int DM>
-static hipError_t launch_cross_grad_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* dkg,
-                                      hipStream_t s) {
-  dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m * h.d);
+static hipError_t launch_cross_fwd_grad_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
+                                          double* dkg, hipStream_t s) {
+  dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m * (1 + h.d));
   const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)cross_grad_plan_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)cross_fwd_grad_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-  hipLaunchKernelGGL(cross_grad_plan_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, dkg, 0);
+  hipLaunchKernelGGL(cross_fwd_grad_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg, dkg,
+                     h.debug_stamp);
   return hipGetLastError();
 }
 
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
                                hipStream_t s) {
   hipError_t e;
-  if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 0)) != hipSuccess) return e;  // Q_X, means; kg = 0
-  if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 1)) != hipSuccess) return e;  // cov rows, variances
-  switch (dim_bucket(h.d)) {                                                            // J_g, dmean; dkg = 0
-    case 2: e = launch_cross_grad_t<2>(h, dev, xnew, B, dkg, s); break;
-    case 4: e = launch_cross_grad_t<4>(h, dev, xnew, B, dkg, s); break;
-    case 8: e = launch_cross_grad_t<8>(h, dev, xnew, B, dkg, s); break;
-    default: e = launch_cross_grad_t<16>(h, dev, xnew, B, dkg, s); break;
+  switch (dim_bucket(h.d)) {  // Q_X (fragment + row-major), means, J_g, dmean; kg = dkg = 0
+    case 2: e = launch_cross_fwd_grad_t<2>(h, dev, xnew, B, kg, dkg, s); break;
+    case 4: e = launch_cross_fwd_grad_t<4>(h, dev, xnew, B, kg, dkg, s); break;
+    case 8: e = launch_cross_fwd_grad_t<8>(h, dev, xnew, B, kg, dkg, s); break;
+    default: e = launch_cross_fwd_grad_t<16>(h, dev, xnew, B, kg, dkg, s); break;
   }
   if (e != hipSuccess) return e;
+  if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 1)) != hipSuccess) return e;  // cov rows, variances
   EnvLaunch a{&h, dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
               envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, h.debug_stamp, xnew, dkg};
   return launch_env<true>(h, a);

@@ -21,21 +21,34 @@ What it restates (reference files, read for behaviour only):
 
 Scalarisation weights are drawn per step with the reference's qMC simplex sampler
 (``bo_loop.py:84-118``, ``dkg_amd.utils.sample_simplex``).
+
+With a ``DataCatalog`` (``dkg_amd.catalog``, the reference's ``pipeline/data_catalog.py`` formats) the
+loop writes what the reference's writes: ``initial_data.pt`` (``bo_loop.py:48-59``), a checkpoint per
+iteration with the surrogate's ``ModelListGP`` state dict (``:281-290, 467-476``), the query history as
+``bo_runs/bo_run_<run_key>.pqt`` in the reference's columns (``:231-255, 388-420``) and the compressed
+checkpoints (``:558-561``); run keys ``eval_separate`` / ``eval_full`` (``main.py:42-43``).
 """
 
 from __future__ import annotations
 
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 from torch import Tensor
 
+from .catalog import DataCatalog
 from .gp_state import DeviceGPState
-from .model import ModelListGPState, SingleTaskGPState
+from .model import ModelListGPState, SingleTaskGPState, to_state_dict
 from .optim import DiscreteKgOptimisationSpec, draw_sobol_samples
 from .utils import sample_simplex
 
 NEVER_FIT_NOISE = 1e-8  # bo_loop.py:583-588
+EVAL_SEPARATE = "eval_separate"  # main.py:42-43
+EVAL_FULL = "eval_full"
+MODEL_CONFIG = {"fit_hyperparams": "never", "kernel": "matern-5/2", "standardize_output": False,
+                "outputs": "one per objective"}
+QUERY_COLUMNS = ("iteration", "x", "obj_index", "obj", "obj_true", "cost", "acq_per_cost", "init", "scalarisation")
 
 
 class GPProblem:
@@ -73,9 +86,12 @@ def surrogate(train_x: Sequence[Tensor], train_y: Sequence[Tensor], hyper: Dict[
 
 def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bool, n_iter: int = 2,
              n_init: int = 6, costs: Sequence[float] = (1, 10), n_scalarisations: int = 16,
-             spec: Optional[DiscreteKgOptimisationSpec] = None, seed: int = 0) -> Dict[str, List]:
+             spec: Optional[DiscreteKgOptimisationSpec] = None, seed: int = 0,
+             catalog: Optional[DataCatalog] = None, run_key: Optional[str] = None) -> Dict[str, List]:
     """``bo_loop.run_mobo`` with the discrete-KG strategy for ``n_iter`` BO steps; returns the
-    query history (x, objective index or None for full evaluation, observed values, acquisition)."""
+    query history (x, objective index or None for full evaluation, observed values, acquisition).
+    With ``catalog`` it also writes the reference's checkpoints and query-history table under
+    ``run_key`` (default ``eval_separate`` / ``eval_full``)."""
     m, d = problem.num_objectives, problem.gp.input_dim
     torch.manual_seed(seed)  # the pipeline's --seed (cli.py): initialize_q_batch's Boltzmann draw
     spec = spec or DiscreteKgOptimisationSpec(n_discretisation_points_per_axis=3, num_restarts=2, raw_samples=4,
@@ -85,9 +101,29 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
     train_x = [x0.clone() for _ in range(m)]
     train_y = [y0[:, i].clone() for i in range(m)]
     hist: Dict[str, List] = {"x": [], "obj_index": [], "obj": [], "acq": [], "cost": []}
+    run_key = run_key or (EVAL_SEPARATE if separate else EVAL_FULL)
+    qh: Dict[str, List] = {k: [] for k in QUERY_COLUMNS}
+
+    def record(iteration, x, i, y, cost, acq_per_cost, init, w):
+        # one row per observed objective value (bo_loop.py:244-255, 388-420); the problem is noise-free
+        for k, v in zip(QUERY_COLUMNS, (iteration, np.asarray(x, dtype=np.float64), i, float(y), float(y),
+                                        float(cost), acq_per_cost, init, w)):
+            qh[k].append(v)
+
+    def checkpoint(iteration, model):
+        if catalog is not None:
+            catalog.save_checkpoint(run_key, iteration, to_state_dict(model), dict(MODEL_CONFIG),
+                                    [t.clone() for t in train_x], [t.clone() for t in train_y],
+                                    [t.clone() for t in train_y], problem.bounds.clone())
+
+    for i in range(m):
+        for j in range(n_init):
+            record(0, x0[j].numpy(), i, y0[j, i], costs[i], float("nan"), True, None)
+    checkpoint(0, surrogate(train_x, train_y, hyper))
     for it in range(n_iter):
         W = sample_simplex(m, n_scalarisations, qmc=True, seed=seed + 1 + it, dtype=torch.double)
         model = surrogate(train_x, train_y, hyper)
+        w_row = W[0].numpy().copy() if W.shape[0] == 1 else None
         if separate:
             x, i, acq = spec.optimize_for_single_objective(model, costs, d, scalarisation_weights=W)
             x = x.reshape(1, d).cpu()
@@ -97,6 +133,7 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
             hist["obj_index"].append(int(i))
             hist["obj"].append(float(y[i]))
             hist["cost"].append(float(costs[i]))
+            record(it + 1, x[0].numpy(), int(i), y[i], costs[i], float(acq), False, w_row)
         else:
             x, acq = spec.optimize_for_full_evaluation(model, d, scalarisation_weights=W)
             x = x.reshape(1, d).cpu()
@@ -107,14 +144,24 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
             hist["obj_index"].append(None)
             hist["obj"].append(y.tolist())
             hist["cost"].append(float(sum(costs)))
+            for i in range(m):
+                record(it + 1, x[0].numpy(), i, y[i], costs[i], float(acq) / float(sum(costs)), False, w_row)
         hist["x"].append(x[0].tolist())
         hist["acq"].append(float(acq))
+        checkpoint(it + 1, surrogate(train_x, train_y, hyper))
     hist["n_observations"] = [int(t.shape[0]) for t in train_x]
+    hist["query_history"] = qh
+    if catalog is not None:
+        import pandas as pd
+
+        catalog.save_bo_run(run_key, pd.DataFrame(qh))
+        catalog.compress_checkpoints(run_key)
     return hist
 
 
-def run_smoke(problem: GPProblem, hyper: Dict[str, Sequence[float]], seed: int = 0) -> Dict[str, Dict]:
+def run_smoke(problem: GPProblem, hyper: Dict[str, Sequence[float]], seed: int = 0,
+              catalog: Optional[DataCatalog] = None) -> Dict[str, Dict]:
     """``run_pipeline`` under ``SMOKE_TEST`` (``main.py:171-216``): the separate-evaluation run and
-    the full-evaluation run, two BO steps each."""
-    return {"separate": run_mobo(problem, hyper, separate=True, seed=seed),
-            "full": run_mobo(problem, hyper, separate=False, seed=seed)}
+    the full-evaluation run, two BO steps each; with ``catalog`` both write the reference's files."""
+    return {"separate": run_mobo(problem, hyper, separate=True, seed=seed, catalog=catalog),
+            "full": run_mobo(problem, hyper, separate=False, seed=seed, catalog=catalog)}

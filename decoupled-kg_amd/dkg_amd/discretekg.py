@@ -226,6 +226,25 @@ class DiscreteKnowledgeGradient(_Base):
         kg = _ForwardFn.apply(Xd, self)
         return kg.to(device=X.device, dtype=X.dtype).reshape(batch_shape)
 
+    def value_and_grad_host(self, X: Tensor):
+        """KG and dKG/dX for host candidates X (``[*batch, 1, d]`` or ``[B, d]``), as host fp64 tensors of
+        shapes ``batch`` and ``X.shape``: what one L-BFGS-B evaluation of ``optimize_acqf`` needs back
+        (``bo_loop.py:127-129``, ``batch_limit = 1``).  The same values and gradient as ``forward`` +
+        autograd, with one device round trip and the launches replayed from a captured graph
+        (``ForwardPlan.forward_grad_host``)."""
+        d = self.x_discretisation.shape[-1]
+        if X.shape[-1] != d:
+            raise RuntimeError(
+                f"Expected X to have last dimension matching 'self.x_discretisation'. "
+                f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
+        if X.dim() > 2 and X.shape[-2] != 1:
+            raise ValueError(f"Expected X to be `batch_shape x q=1 x d`, but got X with shape {tuple(X.shape)}.")
+        self._refresh()
+        flat = X.detach().reshape(-1, d).to("cpu", torch.double)
+        kg, dkg = self._plan_for(flat.shape[0], grad=True).forward_grad_host(flat)
+        batch = X.shape[:-2] if X.dim() > 2 else X.shape[:-1]
+        return kg.reshape(batch), dkg.reshape(X.shape)
+
     def forward_pairs(self, X: Tensor) -> Tensor:
         """KG per (candidate, scalarisation): [B, S] (the per-``j`` values of ``:200-233``)."""
         self._refresh()

@@ -225,6 +225,60 @@ class ForwardPlan:
                    "dkg_plan_forward_grad")
         return kg, dkg
 
+    def forward_grad_host(self, X_host: torch.Tensor, graph: bool = False):
+        """KG[B] and dKG/dx [B, d] for host candidates X (B x d), returned as host tensors: the L-BFGS-B
+        evaluation of ``optimize_acqf`` (``bo_loop.py:127-129``), whose host needs both back every call.
+
+        One pinned H2D copy of X into a plan-owned device buffer, the four launches of
+        ``dkg_plan_forward_grad`` writing KG and dKG/dx side by side into one device buffer, one pinned D2H
+        copy of that buffer and one event wait: a single device round trip instead of one per output.
+        With ``graph`` the launches are a HIP graph captured once per batch size (fixed pointers, so
+        replay is one host call); the results are the same bits as ``forward_grad``."""
+        if not self.grad:
+            raise ValueError("plan was built without grad=True")
+        B, d = X_host.shape[0], self.state.d
+        if X_host.dim() != 2 or X_host.shape[1] != d:
+            raise ValueError(f"X must be B x {d}")
+        if B > self.max_B:
+            raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
+        if B == 0:
+            return torch.empty(0, dtype=torch.double), torch.empty(0, d, dtype=torch.double)
+        if getattr(self, "_hx", None) is None:
+            self._hx = torch.empty(self.max_B * d, dtype=torch.double).pin_memory()
+            self._hout = torch.empty(self.max_B * (d + 1), dtype=torch.double).pin_memory()
+            self._dx = torch.empty(self.max_B * d, dtype=torch.double, device=self.device)
+            self._dout = torch.empty(self.max_B * (d + 1), dtype=torch.double, device=self.device)
+            self._done = torch.cuda.Event()
+            self._graphs = {}
+        hx = self._hx[:B * d].view(B, d)
+        hx.copy_(X_host.detach().reshape(B, d))
+        dx = self._dx[:B * d].view(B, d)
+        kg, dkg = self._dout[:B], self._dout[B:B * (d + 1)].view(B, d)
+        lib = _lib.load()
+
+        def launch(stream):
+            _lib.check(lib.dkg_plan_forward_grad(self.host, self._dev_ptr, _lib.ptr(dx), B, _lib.ptr(kg),
+                                                 _lib.ptr(dkg), stream), "dkg_plan_forward_grad")
+
+        dx.copy_(hx, non_blocking=True)
+        if graph:
+            g = self._graphs.get(B)
+            if g is None:
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    launch(torch.cuda.current_stream(self.device).cuda_stream)
+                self._graphs[B] = g
+                torch.cuda.synchronize(self.device)
+            g.replay()
+        else:
+            launch(current_stream_ptr(self.device))
+        out = self._hout[:B * (d + 1)]
+        out.copy_(self._dout[:B * (d + 1)], non_blocking=True)
+        self._done.record()
+        self._done.synchronize()
+        return out[:B].clone(), out[B:].view(B, d).clone()
+
     def time_stage(self, X: torch.Tensor, stage: int, reps: int) -> float:
         """Average duration (ms) of ``reps`` back-to-back launches of one kernel
         (0 cross_root, 1 posterior_cov, 2 envelope), HIP events on the launch stream."""

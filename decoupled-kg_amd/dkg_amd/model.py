@@ -19,7 +19,7 @@ Three ways in:
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Sequence
+from typing import Dict, List, Sequence
 
 import torch
 
@@ -203,3 +203,37 @@ def from_state_dict(state: dict, train_x, train_y, kernel: str = "matern", nu: f
                                      noise_constraint == "enforced").reshape(-1)[0]),
             mean_constant=c, kernel=kernel, nu=nu, y_mean=y_mean, y_std=y_std))
     return ModelListGPState(*outs)
+
+
+def _inv_softplus(x: torch.Tensor) -> torch.Tensor:
+    """GPyTorch's ``inv_softplus``: the raw value whose softplus is ``x`` (x > 0)."""
+    return x + torch.log(-torch.expm1(-x))
+
+
+def to_state_dict(model: ModelListGPState) -> Dict[str, torch.Tensor]:
+    """The ``ModelListGP.state_dict()`` keys the reference checkpoints (``bo_loop.py:281-290``,
+    ``data_catalog.py:317-348``) for a state built here, in the raw GPyTorch parametrisation that
+    ``from_state_dict(..., noise_constraint="raw")`` reads back: ``Positive`` (softplus) lengthscales and
+    outputscale, the BO loop's ``GreaterThan(..., transform=None)`` noise (``factory.py:95-104``: raw =
+    noise), ``mean_module.raw_constant``, and BoTorch's ``Standardize(m=1)`` buffers when the output is
+    standardised.  ``from_state_dict(to_state_dict(m), train_x, train_y_problem_units, ...)`` rebuilds ``m``
+    (hyperparameters to the last ulp of softplus∘inv_softplus)."""
+    sd: Dict[str, torch.Tensor] = {}
+    f64 = dict(dtype=torch.double)
+    for i, st in enumerate(model.models):
+        p = f"models.{i}."
+        sd[p + "likelihood.noise_covar.raw_noise"] = torch.tensor([st.noise], **f64)
+        sd[p + "likelihood.noise_covar.raw_noise_constraint.lower_bound"] = torch.tensor(0.0, **f64)
+        sd[p + "likelihood.noise_covar.raw_noise_constraint.upper_bound"] = torch.tensor(float("inf"), **f64)
+        sd[p + "mean_module.raw_constant"] = torch.tensor(float(st.mean_constant), **f64)
+        sd[p + "covar_module.raw_outputscale"] = _inv_softplus(torch.tensor(float(st.outputscale), **f64))
+        sd[p + "covar_module.base_kernel.raw_lengthscale"] = _inv_softplus(
+            torch.as_tensor(st.lengthscale, **f64).reshape(1, -1).clone())
+        for k in ("covar_module.raw_outputscale_constraint", "covar_module.base_kernel.raw_lengthscale_constraint"):
+            sd[p + k + ".lower_bound"] = torch.tensor(0.0, **f64)
+            sd[p + k + ".upper_bound"] = torch.tensor(float("inf"), **f64)
+        if st.y_mean != 0.0 or st.y_std != 1.0:
+            sd[p + "outcome_transform.means"] = torch.tensor([[st.y_mean]], **f64)
+            sd[p + "outcome_transform.stdvs"] = torch.tensor([[st.y_std]], **f64)
+            sd[p + "outcome_transform._stdvs_sq"] = torch.tensor([[st.y_std ** 2]], **f64)
+    return sd

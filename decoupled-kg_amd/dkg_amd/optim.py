@@ -105,7 +105,16 @@ def gen_candidates_scipy(initial_conditions: Tensor, acquisition_function: Calla
     ub = upper_bounds.expand(shapeX).reshape(-1).cpu().numpy()
     bounds = list(zip(lb.tolist(), ub.tolist()))
 
+    fast = getattr(acquisition_function, "value_and_grad_host", None)
+
     def f_np(x: np.ndarray):
+        if fast is not None:
+            # the device KG: value and gradient in one round trip (DiscreteKnowledgeGradient.value_and_grad_host)
+            kg, g = fast(torch.from_numpy(x).view(shapeX))
+            loss = -float(kg.sum())
+            if not np.isfinite(loss):
+                raise RuntimeError("acquisition function returned a non-finite value inside L-BFGS-B")
+            return loss, (-g).reshape(-1).numpy()
         X = torch.from_numpy(x).to(ic).view(shapeX).contiguous().requires_grad_(True)
         loss = -acquisition_function(X).sum()
         if not torch.isfinite(loss):

@@ -113,3 +113,39 @@ def test_single_output_model_without_weights():
     b = DiscreteKnowledgeGradient(ModelListGPState(st), D, torch.tensor([[1.0]], dtype=torch.double))
     Xc = torch.rand(5, 1, 2, generator=g, dtype=torch.double)
     assert torch.equal(a(Xc), b(Xc))
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("B", [1, 5, 16])
+def test_value_and_grad_host_matches_forward_and_autograd(B, graph):
+    """value_and_grad_host (one round trip, graph-replayed launches): the same bits as forward + autograd."""
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=1 if B == 5 else None)
+    for rep in range(3):  # repeated calls replay the captured graph on new inputs
+        Xb = X.roll(7 * rep, 0)[:B].clone()
+        Xg = Xb.to(DEV).unsqueeze(-2).requires_grad_(True)
+        kg_ref = acq(Xg)
+        (g_ref,) = torch.autograd.grad(kg_ref.sum(), Xg)
+        plan = acq._plan_for(B, grad=True)
+        kg, g = plan.forward_grad_host(Xb, graph=graph)
+        assert kg.device.type == "cpu" and g.shape == (B, 2)
+        assert torch.equal(kg, kg_ref.detach().cpu())
+        assert torch.equal(g, g_ref.squeeze(-2).cpu())
+        kg2, g2 = acq.value_and_grad_host(Xb.unsqueeze(-2))
+        assert kg2.shape == (B,) and g2.shape == (B, 1, 2)
+        assert torch.equal(kg2, kg) and torch.equal(g2.squeeze(-2), g)
+
+
+def test_value_and_grad_host_follows_a_refit_model():
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W)
+    kg0, _ = acq.value_and_grad_host(X[:1])
+    m0 = model.models[0]
+    model.models[0] = SingleTaskGPState(m0.train_x, m0.train_y, m0.lengthscale * 1.5, m0.outputscale, m0.noise,
+                                        m0.mean_constant, m0.kernel, m0.nu, m0.y_mean, m0.y_std)
+    kg1, g1 = acq.value_and_grad_host(X[:1])
+    Xg = X[:1].to(DEV).unsqueeze(-2).requires_grad_(True)
+    kg_ref = DiscreteKnowledgeGradient(model, D, W)(Xg)
+    (g_ref,) = torch.autograd.grad(kg_ref.sum(), Xg)
+    assert torch.equal(kg1, kg_ref.detach().cpu()) and torch.equal(g1, g_ref.squeeze(-2).cpu())
+    assert not torch.equal(kg0, kg1)

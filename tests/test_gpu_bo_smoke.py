@@ -41,3 +41,38 @@ def test_smoke_pipeline_runs_both_modes():
     # deterministic under the seed
     again = run_smoke(GPProblem(state, device=DEV), HYPER, seed=0)
     assert again["full"]["x"] == full["x"] and again["separate"]["x"] == sep["x"]
+
+
+def test_smoke_pipeline_writes_the_reference_catalog(tmp_path):
+    """With a DataCatalog the loop writes the reference's files (data_catalog.py layout): the query history
+    table in the reference's columns, one checkpoint per iteration (compressed at the end), and the
+    checkpointed state dict rebuilds the surrogate the loop used (same KG on the device)."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.bo_smoke import QUERY_COLUMNS, surrogate
+    from dkg_amd.catalog import DataCatalog
+    from dkg_amd.model import from_state_dict
+
+    state, *_ = load_golden("lengthscales0")
+    cat = DataCatalog("smoke", data_dir=str(tmp_path))
+    res = run_smoke(GPProblem(state, device=DEV), HYPER, seed=0, catalog=cat)
+    plain = run_smoke(GPProblem(state, device=DEV), HYPER, seed=0)
+    assert res["full"]["x"] == plain["full"]["x"] and res["separate"]["x"] == plain["separate"]["x"]
+    for key, mode in (("eval_separate", "separate"), ("eval_full", "full")):
+        df = cat.load_bo_run(key)
+        assert tuple(df.columns) == QUERY_COLUMNS
+        n_new = 2 if mode == "separate" else 2 * 2
+        assert len(df) == 2 * 6 + n_new and int(df["init"].sum()) == 12
+        assert df["iteration"].max() == 2
+        cat.uncompress_checkpoints(key)
+        assert cat.num_checkpoints(key) == 3
+        ck = cat.load_checkpoint(key, -1)
+        assert ck["iteration"] == 2 and ck["model_config"]["fit_hyperparams"] == "never"
+        assert [int(t.shape[0]) for t in ck["train_x"]] == res[mode]["n_observations"]
+        rebuilt = from_state_dict(ck["model_state_dict"], ck["train_x"], ck["train_obj"], noise_constraint="raw")
+        direct = surrogate(ck["train_x"], ck["train_obj"], HYPER)
+        D = torch.rand(64, 2, dtype=torch.double, generator=torch.Generator().manual_seed(1))
+        W = torch.tensor([[0.3, 0.7], [0.6, 0.4]], dtype=torch.double)
+        Xc = torch.rand(8, 1, 2, dtype=torch.double, generator=torch.Generator().manual_seed(2))
+        kg_a = DiscreteKnowledgeGradient(rebuilt, D, W)(Xc.to(DEV))
+        kg_b = DiscreteKnowledgeGradient(direct, D, W)(Xc.to(DEV))
+        torch.testing.assert_close(kg_a, kg_b, rtol=1e-9, atol=1e-15)

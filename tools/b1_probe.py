@@ -1,0 +1,80 @@
+"""Where the B = 1 value+gradient latency goes (the reference's optimize_acqf call shape, bo_loop.py:127-129).
+
+Run on the GPU box from the repo root:  python tools/b1_probe.py [workload] [calls]
+Prints median microseconds per call for:
+  launch   -- host time of the C call alone (4 launches), no sync
+  device   -- back-to-back calls, HIP events on the stream (device-bound per-call time)
+  bench    -- forward_grad + kg.cpu() + dkg.cpu() (bench.py's latency_b1 leg)
+  fused    -- forward_grad_host(): one pinned H2D, the C call, one pinned D2H of [kg, dkg], one event sync
+  graph    -- the same with the four launches replayed from a captured HIP graph
+"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "decoupled-kg_amd")]
+import torch  # noqa: E402
+
+from dkg_amd import DiscreteKnowledgeGradient  # noqa: E402
+from dkg_amd.synthetic import WORKLOADS, make_problem  # noqa: E402
+
+
+def med(ts):
+    ts = sorted(ts)
+    return round(ts[len(ts) // 2] * 1e6, 1)
+
+
+w = WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "headline"]
+calls = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+model, D, X, W = make_problem(w)
+acq = DiscreteKnowledgeGradient(model, D, W)
+p1 = acq._plan_for(1, grad=True)
+Xd = X.cuda().contiguous()
+xs = [Xd[i % w.B:i % w.B + 1].contiguous() for i in range(calls)]
+xh = [x.cpu() for x in xs]
+for i in range(10):
+    p1.forward_grad(xs[i])
+torch.cuda.synchronize()
+
+res = {}
+ts = []
+for i in range(calls):
+    t0 = time.perf_counter()
+    p1.forward_grad(xs[i])
+    ts.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+res["launch"] = med(ts)
+
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for i in range(calls):
+    p1.forward_grad(xs[i])
+e1.record()
+torch.cuda.synchronize()
+res["device"] = round(e0.elapsed_time(e1) * 1e3 / calls, 1)
+
+ts = []
+for i in range(calls):
+    t0 = time.perf_counter()
+    kg, g = p1.forward_grad(xs[i])
+    kg.cpu(), g.cpu()
+    ts.append(time.perf_counter() - t0)
+res["bench"] = med(ts)
+
+ref = [p1.forward_grad(xs[i]) for i in range(8)]
+ref = [(a.cpu(), b.cpu()) for a, b in ref]
+if hasattr(p1, "forward_grad_host"):
+    for graph in (False, True):
+        for i in range(10):
+            p1.forward_grad_host(xh[i], graph=graph)
+        ok = all(torch.equal(p1.forward_grad_host(xh[i], graph=graph)[0], ref[i][0])
+                 and torch.equal(p1.forward_grad_host(xh[i], graph=graph)[1], ref[i][1]) for i in range(8))
+        ts = []
+        for i in range(calls):
+            t0 = time.perf_counter()
+            p1.forward_grad_host(xh[i], graph=graph)
+            ts.append(time.perf_counter() - t0)
+        res["graph" if graph else "fused"] = med(ts)
+        res[("graph" if graph else "fused") + "_bit_identical"] = ok
+print(res)
