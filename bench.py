@@ -423,7 +423,7 @@ def main():
         if args.b1_calls > 0:
             # B = 1: the reference's production call shape (bo_loop.py:127-129), one synchronous C call
             # per L-BFGS-B evaluation; the host needs the value and gradient back each time
-            # value_and_grad_host: host x in, host (KG, dKG/dx) out, one round trip, graph-replayed launches
+            # value_and_grad_host: host x in, host (KG, dKG/dx) out, one round trip
             p1 = acq._plan_for(1, grad=True)
             xh = tp.Xd.cpu()
             for i in range(5):
@@ -445,8 +445,10 @@ def main():
             te.sort()
             lat_b1 = {"median_us": ts[len(ts) // 2] * 1e6, "p90_us": ts[int(len(ts) * 0.9)] * 1e6,
                       "calls": len(ts), "eager_two_copies_median_us": te[len(te) // 2] * 1e6,
-                      "what": "value + dKG/dx at one host candidate (value_and_grad_host: pinned H2D, graph "
-                              "replay of the 4 launches, one pinned D2H), device round trip included"}
+                      "what": "value + dKG/dx at one host candidate through the public entry the L-BFGS-B "
+                              "objective calls (value_and_grad_host: model check, pinned H2D, 3 launches, one "
+                              "pinned D2H), device round trip included; eager_two_copies: the plan's C call on a "
+                              "device candidate + two .cpu() copies"}
 
     # ---- non-degenerate leg: headline sizes, KG > 0 for every pair (workload headline_nd, d = 6)
     nd = None

@@ -80,11 +80,12 @@ def _fingerprint(obj):
     whenever this changes (a refit, new training data, an in-place edit)."""
     if isinstance(obj, torch.Tensor):
         return (id(obj), obj._version)
-    if isinstance(obj, ModelListGPState):
-        return tuple(_fingerprint(m) for m in obj.models)
+    if isinstance(obj, ModelListGPState):  # flat, no recursion: this runs on every forward
+        return tuple((id(m.train_x), m.train_x._version, id(m.train_y), m.train_y._version, id(m.lengthscale),
+                      m.lengthscale._version, m.outputscale, m.noise, m.mean_constant, m.kernel, m.nu, m.y_mean,
+                      m.y_std) for m in obj.models)
     if isinstance(obj, SingleTaskGPState):
-        return (_fingerprint(obj.train_x), _fingerprint(obj.train_y), _fingerprint(obj.lengthscale),
-                obj.outputscale, obj.noise, obj.mean_constant, obj.kernel, obj.nu, obj.y_mean, obj.y_std)
+        return _fingerprint(ModelListGPState(obj))
     if isinstance(obj, torch.nn.Module):  # a BoTorch model: parameters, buffers and training data
         parts = [_fingerprint(t) for t in obj.parameters()] + [_fingerprint(t) for t in obj.buffers()]
         for sub in getattr(obj, "models", None) or [obj]:
@@ -240,7 +241,9 @@ class DiscreteKnowledgeGradient(_Base):
         if X.dim() > 2 and X.shape[-2] != 1:
             raise ValueError(f"Expected X to be `batch_shape x q=1 x d`, but got X with shape {tuple(X.shape)}.")
         self._refresh()
-        flat = X.detach().reshape(-1, d).to("cpu", torch.double)
+        flat = X.detach().reshape(-1, d)
+        if flat.dtype != torch.double or flat.device.type != "cpu":
+            flat = flat.to("cpu", torch.double)
         kg, dkg = self._plan_for(flat.shape[0], grad=True).forward_grad_host(flat)
         batch = X.shape[:-2] if X.dim() > 2 else X.shape[:-1]
         return kg.reshape(batch), dkg.reshape(X.shape)
