@@ -31,6 +31,7 @@ Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus
 """
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -157,6 +158,30 @@ def cpu_baseline(model, D, W, X, target, seconds, threads_req):
                       f"{threads} threads), {dt:.1f} s"}
 
 
+def hip_runtime():
+    """The HIP runtime instance torch already loaded (hipGraphLaunch for the per-stream graph replays): opened
+    by the path it is mapped from, so no second copy of the runtime is loaded."""
+    path = "libamdhip64.so.7"
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line and line.strip().split()[-1].startswith("/"):
+                path = line.strip().split()[-1]
+                break
+    lib = ctypes.CDLL(path)
+    for name, args in (("hipGraphLaunch", [ctypes.c_void_p, ctypes.c_void_p]),
+                       ("hipEventCreateWithFlags", [ctypes.c_void_p, ctypes.c_uint]),
+                       ("hipEventRecord", [ctypes.c_void_p, ctypes.c_void_p]),
+                       ("hipStreamWaitEvent", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint])):
+        getattr(lib, name).argtypes = args
+        getattr(lib, name).restype = ctypes.c_int
+    return lib
+
+
+def hip_check(rc: int, what: str) -> None:
+    if rc:
+        raise RuntimeError(f"{what} failed: HIP error {rc}")
+
+
 class Throughput:
     """The timed throughput path: E forward batches per exchange, ``streams`` batches in flight, one
     captured HIP graph per exchange buffer (DESIGN.md §6 "Forward batches in flight")."""
@@ -212,6 +237,16 @@ class Throughput:
                     gs.append(g)
                 graphs.append(gs)
             torch.cuda.synchronize()
+            # replayed with hipGraphLaunch on the raw executable graphs (what CUDAGraph.replay calls, without
+            # its Python and stream-guard overhead: ~9 instead of ~18 us of host time per launch, which is
+            # what a short run's four launches cost before the last stream starts)
+            hip = hip_runtime()
+            execs = [[ctypes.c_void_p(g.raw_cuda_graph_exec()) for g in gs] for gs in graphs]
+            sptrs = [ctypes.c_void_p(s.cuda_stream) for s in streams]
+            # the fork / join events, created once (torch's wait_stream creates an event per call)
+            evs = [ctypes.c_void_p() for _ in range(ns)]
+            for e in evs:
+                hip_check(hip.hipEventCreateWithFlags(ctypes.byref(e), 2), "hipEventCreateWithFlags")  # no timing
         elif graph and steps >= E:
             # one graph per exchange buffer: the E forwards of a period, forked over the streams exactly
             # as the eager path does; replayed on the main stream, so the collective after it orders as before
@@ -242,8 +277,9 @@ class Throughput:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record()
-        for s in streams[1:]:
-            s.wait_stream(main_s)
+        if not graphs:
+            for s in streams[1:]:
+                s.wait_stream(main_s)
         k0 = 0
         host = 0.0  # host seconds inside the launch calls (replay / plan.forward_into)
         if graphs:
@@ -252,12 +288,15 @@ class Throughput:
                 th = time.perf_counter()
                 g = graphs[(k0 // E) % 2]
                 if graph == 2:
-                    for s in streams[1:]:
-                        s.wait_stream(main_s)
-                    for i in range(ns):
-                        with torch.cuda.stream(streams[i]):
-                            g[i].replay()
-                    join()
+                    # fork: every stream after the main stream's work so far; one graph per stream; join
+                    hip_check(hip.hipEventRecord(evs[0], sptrs[0]), "hipEventRecord")
+                    for i in range(1, ns):
+                        hip_check(hip.hipStreamWaitEvent(sptrs[i], evs[0], 0), "hipStreamWaitEvent")
+                    for i, ex in enumerate(execs[(k0 // E) % 2]):
+                        hip_check(hip.hipGraphLaunch(ex, sptrs[i]), "hipGraphLaunch")
+                    for i in range(1, ns):
+                        hip_check(hip.hipEventRecord(evs[i], sptrs[i]), "hipEventRecord")
+                        hip_check(hip.hipStreamWaitEvent(sptrs[0], evs[i], 0), "hipStreamWaitEvent")
                 else:
                     g.replay()
                 host += time.perf_counter() - th
