@@ -288,10 +288,12 @@ class Throughput:
                 th = time.perf_counter()
                 g = graphs[(k0 // E) % 2]
                 if graph == 2:
-                    # fork: every stream after the main stream's work so far; one graph per stream; join
-                    hip_check(hip.hipEventRecord(evs[0], sptrs[0]), "hipEventRecord")
-                    for i in range(1, ns):
-                        hip_check(hip.hipStreamWaitEvent(sptrs[i], evs[0], 0), "hipStreamWaitEvent")
+                    # fork: every stream after the main stream's work so far (the previous period's exchange);
+                    # the first period starts on an idle device (synchronized above), so it needs none
+                    if k0 > 0:
+                        hip_check(hip.hipEventRecord(evs[0], sptrs[0]), "hipEventRecord")
+                        for i in range(1, ns):
+                            hip_check(hip.hipStreamWaitEvent(sptrs[i], evs[0], 0), "hipStreamWaitEvent")
                     for i, ex in enumerate(execs[(k0 // E) % 2]):
                         hip_check(hip.hipGraphLaunch(ex, sptrs[i]), "hipGraphLaunch")
                     for i in range(1, ns):
