@@ -1468,7 +1468,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
       } else {
         double la[MAXL], lb[MAXL];
         build_lines(la, lb);
-        f = envelope_filter<MAXL, true>(la, lb, lane, sb, sa, si);
+        // Flat envelope (env_flat, as in the forward): every breakpoint beyond +-48, so every phi / psi
+        // term is exactly 0 and every Phi exactly 0 or 1: KG_w = 0 and the pair's gradient terms cancel to
+        // exactly 0 (line 0 off the top: no da_0 term; line 0 = T: Phi(cR) - Phi(cL) = 1 against the
+        // [line 0 attains max a] / cnt term with cnt = 1).  Only an exact copy of line 0 at the top (cnt > 1,
+        // a subgradient share) needs the full path.
+        bool flat = false;
+        if (!force_walk) {
+          FwdEnv fe;
+          env_top<MAXL>(la, lb, fe);
+          if (env_flat<MAXL>(la, lb, fe)) {
+            const double a0l = readlane_f64(la[0], 0);
+            int ct = 0;
+#pragma unroll
+            for (int t = 0; t < MAXL; ++t) ct += __popcll(ballot(la[t] == fe.aT));
+            flat = !(a0l == fe.aT) || ct == 1;
+          }
+        }
+        if (flat)
+          f.status = 3;
+        else
+          f = envelope_filter<MAXL, true>(la, lb, lane, sb, sa, si);
       }
       if (force_walk && f.status == 0) f.status = 2;
       if (j == j0 + wave) KST(st, 3);
@@ -1674,7 +1694,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
         f.kR = __builtin_amdgcn_readfirstlane(kR);
         f.cntT = ct;
       }
-      if (f.status == 1) {
+      if (f.status == 1 || f.status == 3) {  // short-circuit, flat envelope: KG_w = 0, no gradient terms
         kgj = 0.0;
       } else {
         if (f.status == 0) {
