@@ -173,3 +173,25 @@ def test_overflow_walk_path_value_and_grad(workload, target):
     assert (kg - kg_ref).abs().max().item() <= 1e-6 * scale + 1e-15
     assert (kg2.cpu() - kg_ref).abs().max().item() <= 1e-6 * scale + 1e-15
     assert_grad_close(g.cpu(), g_ref)
+
+
+@pytest.mark.parametrize("target", [None, 1])
+def test_flat_early_out_matches_the_full_gradient_path(target):
+    """The gradient envelope settles flat pairs (every breakpoint beyond +-48) without the filter and hull:
+    KG and dKG/dx against the full path (DKG_PLAN_FORCE_WALK, no early-out) on the headline batch, where 89 %
+    of the pairs are flat, plus candidates placed on discretisation points (line 0 duplicated by a line k)."""
+    model, D, X, W = make_problem(WORKLOADS["headline"])
+    X = X.clone()
+    X[:8] = D[torch.tensor([0, 37, 100, 333, 512, 700, 901, 1023])]
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    Xd = X.to(DEV).contiguous()
+    kg, g = acq._plan_for(X.shape[0], grad=True).forward_grad(Xd)
+    full = acq._state.plan(acq._W, acq._target, X.shape[0], grad=True, force_walk=True)
+    kg_f, g_f = full.forward_grad(Xd)
+    torch.testing.assert_close(kg, kg_f, rtol=1e-12, atol=0.0)
+    assert_grad_close(g.cpu(), g_f.cpu())
+    # off the discretisation, KG = 0 leaves at most denormal-scale gradient terms (breakpoints at 37-40
+    # standard deviations, where psi rounds to 0 before phi does) on either path
+    zero = kg_f == 0
+    zero[:8] = False
+    assert float(g[zero].abs().max()) <= 1e-250 and float(g_f[zero].abs().max()) <= 1e-250
