@@ -229,7 +229,7 @@ class ForwardPlan:
         """KG[B] and dKG/dx [B, d] for host candidates X (B x d), returned as host tensors: the L-BFGS-B
         evaluation of ``optimize_acqf`` (``bo_loop.py:127-129``), whose host needs both back every call.
 
-        One pinned H2D copy of X into a plan-owned device buffer, the four launches of
+        One pinned H2D copy of X into a plan-owned device buffer, the three launches of
         ``dkg_plan_forward_grad`` writing KG and dKG/dx side by side into one device buffer, one pinned D2H
         copy of that buffer and one event wait: a single device round trip instead of one per output.
         With ``graph`` the launches are a HIP graph captured once per batch size (fixed pointers, so

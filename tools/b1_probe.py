@@ -2,11 +2,11 @@
 
 Run on the GPU box from the repo root:  python tools/b1_probe.py [workload] [calls]
 Prints median microseconds per call for:
-  launch   -- host time of the C call alone (4 launches), no sync
+  launch   -- host time of the C call alone (3 launches), no sync
   device   -- back-to-back calls, HIP events on the stream (device-bound per-call time)
   bench    -- forward_grad + kg.cpu() + dkg.cpu() (bench.py's latency_b1 leg)
   fused    -- forward_grad_host(): one pinned H2D, the C call, one pinned D2H of [kg, dkg], one event sync
-  graph    -- the same with the four launches replayed from a captured HIP graph
+  graph    -- the same with the three launches replayed from a captured HIP graph
 """
 import os
 import sys
