@@ -648,6 +648,7 @@ __global__ __launch_bounds__(256) void lines_kg_kernel(const double* __restrict_
     if (kg) kg[p] = v;
     if (nhull) nhull[p] = h;
   }
+  if (idx) pad_walk_out(out, h, lane);
 }
 
 // Epigraph of line sets too long for the register path (L > 64 * 33): the
@@ -698,6 +699,7 @@ __global__ __launch_bounds__(256) void lines_walk_kernel(const double* __restric
     if (kg) kg[p] = v;
     if (nhull) nhull[p] = h;
   }
+  if (idx) pad_walk_out(out, h, lane);
 }
 
 // ---------------------------------------------------------------------------

@@ -104,6 +104,13 @@ struct WalkOut {
   int cap;
 };
 
+// After the accepted walk of h lines: indices h .. cap-1 = -1 and intersections h-1 .. cap-2 = NaN (a list
+// walk rejected for a breakpoint beyond its guard, and redone, may have written past the final count).
+__device__ __forceinline__ void pad_walk_out(const WalkOut& out, int h, int lane) {
+  for (int e = h + lane; e < out.cap; e += 64) out.idx[e] = -1;
+  for (int e = (h > 0 ? h - 1 : 0) + lane; e < out.cap - 1; e += 64) out.x[e] = __builtin_nan("");
+}
+
 // The KG edge terms a walk leaves for the single psi evaluation of its caller
 // (finish_edges): `kg` is the part already summed (walks of more than 64
 // steps flush every 64), and each lane with `on` holds one pending edge

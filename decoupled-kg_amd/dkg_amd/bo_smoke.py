@@ -46,8 +46,28 @@ from .utils import sample_simplex
 NEVER_FIT_NOISE = 1e-8  # bo_loop.py:583-588
 EVAL_SEPARATE = "eval_separate"  # main.py:42-43
 EVAL_FULL = "eval_full"
-MODEL_CONFIG = {"fit_hyperparams": "never", "kernel": "matern-5/2", "standardize_output": False,
-                "outputs": "one per objective"}
+
+
+def _output_config(lengthscale_rate: float) -> dict:
+    return {"likelihood": {"type": "gaussian", "noise_prior": {"type": "gamma", "args": {"concentration": 1.1,
+                                                                                        "rate": 0.05}}},
+            "fix_zero_noise": True,
+            "kernel": {"type": "matern", "ard": True, "args": {"nu": 2.5},
+                       "lengthscale_prior": {"type": "gamma", "args": {"concentration": 3, "rate": lengthscale_rate}},
+                       "outputscale_prior": {"type": "gamma", "args": {"concentration": 2, "rate": 0.15}}},
+            "standardize_output": False}
+
+
+def reference_model_config(m: int, bounds) -> dict:
+    """The ``model_config`` the reference's SMOKE run checkpoints (``bo_loop.py:281-290``): the ``model``
+    section of ``config/experiment-lengthscales.yaml`` (the ``gp-sample:lengthscales`` problem), completed
+    as ``pipeline/cli.py:22-37`` does for ``--fit-hyperparams never`` (``fit_hyperparams``, and
+    ``standardize_output = False`` per output), with the problem's bounds.  ``build_mll_and_model``
+    (``factory.py:24-60``) reads ``bounds``, ``fit_hyperparams`` and ``outputs[i]`` from it.  Outputs past
+    the config's two repeat its second output's section.  Pinned by tests/golden/ref_schema.json."""
+    bnd = torch.as_tensor(bounds, dtype=torch.double).reshape(2, -1)
+    return {"bounds": bnd.tolist(), "outputs": [_output_config(10 if i == 0 else 1.1) for i in range(m)],
+            "fit_hyperparams": "never"}
 QUERY_COLUMNS = ("iteration", "x", "obj_index", "obj", "obj_true", "cost", "acq_per_cost", "init", "scalarisation")
 
 
@@ -58,7 +78,7 @@ class GPProblem:
     def __init__(self, gp: ModelListGPState, bounds: Optional[Tensor] = None, device=None):
         self.gp = gp
         d = gp.input_dim
-        self.bounds = (torch.stack([torch.zeros(d), torch.ones(d)]) if bounds is None
+        self.bounds = (torch.stack([torch.zeros(d, dtype=torch.double), torch.ones(d, dtype=torch.double)]) if bounds is None
                        else torch.as_tensor(bounds, dtype=torch.double).reshape(2, d))
         self.device = device
         self.num_objectives = gp.num_outputs
@@ -78,7 +98,7 @@ def surrogate(train_x: Sequence[Tensor], train_y: Sequence[Tensor], hyper: Dict[
               noise: float = NEVER_FIT_NOISE) -> ModelListGPState:
     """The BO model on the observations so far, one output per objective with its own data
     (decoupled evaluations give every objective its own training set), fixed hyperparameters."""
-    outs = [SingleTaskGPState(train_x[i], train_y[i], torch.tensor(hyper["length_scales"][i]),
+    outs = [SingleTaskGPState(train_x[i], train_y[i], torch.tensor(hyper["length_scales"][i], dtype=torch.double),
                               float(hyper["output_scales"][i]), noise, float(hyper["means"][i]))
             for i in range(len(train_x))]
     return ModelListGPState(*outs)
@@ -93,10 +113,15 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
     With ``catalog`` it also writes the reference's checkpoints and query-history table under
     ``run_key`` (default ``eval_separate`` / ``eval_full``)."""
     m, d = problem.num_objectives, problem.gp.input_dim
-    torch.manual_seed(seed)  # the pipeline's --seed (cli.py): initialize_q_batch's Boltzmann draw
+    # the pipeline's --seed (main.py:235, utils.set_random_seed): every later draw comes from the global RNG, as
+    # in the reference -- the initial Sobol points (generate_initial_data, bo_loop.py:48-49: no seed), each
+    # optimize_acqf's raw-sample Sobol seed (options without "seed", acquisition_optimisation_strategy.py:217-224)
+    # and initialize_q_batch's Boltzmann draw.  (A fixed raw-sample seed equal to the initial data's would make
+    # the raw samples the training points, where the KG is 0.)
+    torch.manual_seed(seed)
     spec = spec or DiscreteKgOptimisationSpec(n_discretisation_points_per_axis=3, num_restarts=2, raw_samples=4,
-                                              batch_limit=1, max_iter=200, device=problem.device, seed=seed)
-    x0 = draw_sobol_samples(problem.bounds, n_init, 1, seed=seed).squeeze(-2)
+                                              batch_limit=1, max_iter=200, device=problem.device)
+    x0 = draw_sobol_samples(problem.bounds, n_init, 1).squeeze(-2)
     y0 = problem(x0)
     train_x = [x0.clone() for _ in range(m)]
     train_y = [y0[:, i].clone() for i in range(m)]
@@ -110,9 +135,11 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
                                         float(cost), acq_per_cost, init, w)):
             qh[k].append(v)
 
+    model_config = reference_model_config(m, problem.bounds)
+
     def checkpoint(iteration, model):
         if catalog is not None:
-            catalog.save_checkpoint(run_key, iteration, to_state_dict(model), dict(MODEL_CONFIG),
+            catalog.save_checkpoint(run_key, iteration, to_state_dict(model, model_config), model_config,
                                     [t.clone() for t in train_x], [t.clone() for t in train_y],
                                     [t.clone() for t in train_y], problem.bounds.clone())
 

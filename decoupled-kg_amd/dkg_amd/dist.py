@@ -93,6 +93,27 @@ class _AllGather(torch.autograd.Function):
         return g[ctx.rank * ctx.n:(ctx.rank + 1) * ctx.n], None, None, None
 
 
+class _ZerosConnected(torch.autograd.Function):
+    """Zeros [n] on ``cdev`` that stay in the autograd graph of ``x`` (a rank with no local work must
+    still join the collective backward); the backward hands ``x`` an exact zero gradient, so a
+    non-finite coordinate in ``x`` cannot leak into the zeros (``0 * inf`` would be NaN)."""
+
+    @staticmethod
+    def forward(ctx, x, n, cdev):
+        ctx.shape, ctx.dtype, ctx.device = x.shape, x.dtype, x.device
+        return torch.zeros(n, dtype=torch.double, device=cdev)
+
+    @staticmethod
+    def backward(ctx, g):
+        return torch.zeros(ctx.shape, dtype=ctx.dtype, device=ctx.device), None, None
+
+
+def _zeros_like_graph(x: Tensor, n: int, cdev: torch.device) -> Tensor:
+    if x.requires_grad:
+        return _ZerosConnected.apply(x, n, cdev)
+    return torch.zeros(n, dtype=torch.double, device=cdev)
+
+
 def shard_range(total: int, rank: int, world: int) -> tuple:
     """Contiguous slice [lo, hi) of ``total`` items owned by ``rank`` (chunks of ceil(total/world))."""
     chunk = -(-total // world) if total > 0 else 0
@@ -159,7 +180,7 @@ class ShardedDiscreteKG:
             if n_local > 0 and B > 0:
                 part = self._local(flat, self.W[self.w_lo:self.w_hi]).to(cdev, torch.double) * n_local
             else:
-                part = torch.zeros(B, dtype=torch.double, device=cdev) + 0.0 * flat.sum().to(cdev, torch.double)
+                part = _zeros_like_graph(flat, B, cdev)
             if self.world > 1:
                 part = _AllReduceSum.apply(part, self.group)
             out = part / self.S
@@ -171,13 +192,62 @@ class ShardedDiscreteKG:
                 pieces.append(self._local(flat[lo:hi], self.W).to(cdev, torch.double))
             pad = chunk - (hi - lo)
             if pad > 0 or not pieces:
-                pieces.append(torch.zeros(pad, dtype=torch.double, device=cdev) + 0.0 * flat.sum().to(cdev, torch.double))
+                pieces.append(_zeros_like_graph(flat, pad, cdev))
             mine = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
             allv = _AllGather.apply(mine, self.world, self.rank, self.group) if self.world > 1 else mine
             out = allv[:B]
         return out.to(X.device).reshape(batch_shape)
 
     __call__ = forward
+
+    def forward_async(self, X: Tensor) -> "PendingKG":
+        """The no-grad forward with its exchange left in flight: the local evaluation is enqueued and the
+        collective started asynchronously (``async_op=True``), so a caller evaluating many batches (the
+        raw-sample scoring of ``optimize_acqf``, bench.py) can issue the next batch before this one's
+        collective completes.  ``.wait()`` returns what ``forward`` returns.  The gradient path stays
+        synchronous (its backward is a collective too)."""
+        if X.dim() < 2 or X.shape[-2] != 1:
+            raise AssertionError(f"Expected X to be `batch_shape x q=1 x d`, but got X with shape {X.shape}.")
+        batch_shape = X.shape[:-2]
+        flat = X.detach().reshape(-1, self.d)
+        B = flat.shape[0]
+        cdev = self._comm_device(flat)
+        if self.axis == "scalarisations":
+            n_local = self.w_hi - self.w_lo
+            if n_local > 0 and B > 0:
+                buf = (self._local(flat, self.W[self.w_lo:self.w_hi]).detach().to(cdev, torch.double) * n_local)
+            else:
+                buf = torch.zeros(B, dtype=torch.double, device=cdev)
+            buf = buf.contiguous()
+            work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True) \
+                if self.world > 1 else _Done()
+            return PendingKG(work, lambda: (buf / self.S).to(X.device).reshape(batch_shape))
+        chunk = -(-B // self.world) if B > 0 else 0
+        lo, hi = shard_range(B, self.rank, self.world)
+        mine = torch.zeros(chunk, dtype=torch.double, device=cdev)
+        if hi > lo:
+            mine[:hi - lo] = self._local(flat[lo:hi], self.W).detach().to(cdev, torch.double)
+        if self.world == 1:
+            return PendingKG(_Done(), lambda: mine[:B].to(X.device).reshape(batch_shape))
+        allv = torch.empty(chunk * self.world, dtype=torch.double, device=cdev)
+        if cdev.type == "cuda":
+            work = dist.all_gather_into_tensor(allv, mine, group=self.group, async_op=True)
+        else:
+            work = dist.all_gather(list(allv.view(self.world, -1)), mine, group=self.group, async_op=True)
+        return PendingKG(work, lambda: allv[:B].to(X.device).reshape(batch_shape))
+
+
+class PendingKG:
+    """An exchange in flight (ShardedDiscreteKG.forward_async); ``wait()`` completes it and returns the KG."""
+
+    def __init__(self, work, result: Callable[[], Tensor]):
+        self._work, self._result, self._out = work, result, None
+
+    def wait(self) -> Tensor:
+        if self._out is None:
+            self._work.wait()
+            self._out = self._result()
+        return self._out
 
 
 class BatchExchange:

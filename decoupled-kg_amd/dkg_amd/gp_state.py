@@ -229,11 +229,13 @@ class ForwardPlan:
         """KG[B] and dKG/dx [B, d] for host candidates X (B x d), returned as host tensors: the L-BFGS-B
         evaluation of ``optimize_acqf`` (``bo_loop.py:127-129``), whose host needs both back every call.
 
-        One pinned H2D copy of X into a plan-owned device buffer, the three launches of
-        ``dkg_plan_forward_grad`` writing KG and dKG/dx side by side into one device buffer, one pinned D2H
-        copy of that buffer and one event wait: a single device round trip instead of one per output.
-        With ``graph`` the launches are a HIP graph captured once per batch size (fixed pointers, so
-        replay is one host call); the results are the same bits as ``forward_grad``."""
+        One pinned H2D copy of X into a plan-owned device buffer, the launches of ``dkg_plan_forward_grad``
+        (eager, the default) writing KG and dKG/dx side by side into one device buffer, one pinned D2H copy
+        of that buffer and one event wait: a single device round trip instead of one per output.  Everything
+        is ordered on the current stream of the plan's device (which need not be the current device), and
+        the completion event is recorded there.  With ``graph`` the launches are a HIP graph captured once
+        per batch size (fixed pointers, so replay is one host call; measured slower than eager launches at
+        B = 1); the results are the same bits as ``forward_grad``."""
         if not self.grad:
             raise ValueError("plan was built without grad=True")
         B, d = X_host.shape[0], self.state.d
@@ -243,6 +245,12 @@ class ForwardPlan:
             raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
         if B == 0:
             return torch.empty(0, dtype=torch.double), torch.empty(0, d, dtype=torch.double)
+        with torch.cuda.device(self.device):
+            return self._forward_grad_host(X_host, B, d, graph)
+
+    def _forward_grad_host(self, X_host: torch.Tensor, B: int, d: int, graph: bool):
+        # runs with the plan's device current: the copies, the launches and the event share its stream
+        stream = torch.cuda.current_stream(self.device)
         if getattr(self, "_hx", None) is None:
             self._hx = torch.empty(self.max_B * d, dtype=torch.double).pin_memory()
             self._hout = torch.empty(self.max_B * (d + 1), dtype=torch.double).pin_memory()
@@ -272,10 +280,10 @@ class ForwardPlan:
                 torch.cuda.synchronize(self.device)
             g.replay()
         else:
-            launch(current_stream_ptr(self.device))
+            launch(stream.cuda_stream)
         out = self._hout[:B * (d + 1)]
         out.copy_(self._dout[:B * (d + 1)], non_blocking=True)
-        self._done.record()
+        self._done.record(stream)
         self._done.synchronize()
         return out[:B].clone(), out[B:].view(B, d).clone()
 

@@ -19,7 +19,7 @@ Three ways in:
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -210,21 +210,57 @@ def _inv_softplus(x: torch.Tensor) -> torch.Tensor:
     return x + torch.log(-torch.expm1(-x))
 
 
-def to_state_dict(model: ModelListGPState) -> Dict[str, torch.Tensor]:
-    """The ``ModelListGP.state_dict()`` keys the reference checkpoints (``bo_loop.py:281-290``,
+# factory.py:15-20: the noise floor of a fitted / a fixed-hyperparameter ("never") surrogate
+MIN_NOISE_SE = 1e-2
+MIN_NOISE_SE_FIXED = 1e-4
+
+
+def _prior_buffers(prior_cfg) -> Dict[str, float]:
+    """The buffers of a prior the reference's config names (``factory.py:138-151``: only ``gamma``):
+    gpytorch's ``GammaPrior`` registers ``concentration`` and ``rate``."""
+    if prior_cfg is None:
+        return {}
+    if prior_cfg["type"] != "gamma":
+        raise ValueError(f"Unsupported prior 'type'. Got {prior_cfg['type']!r}.")
+    return {"concentration": float(prior_cfg["args"]["concentration"]), "rate": float(prior_cfg["args"]["rate"])}
+
+
+def to_state_dict(model: ModelListGPState, model_config: Optional[dict] = None) -> Dict[str, torch.Tensor]:
+    """The ``ModelListGP.state_dict()`` the reference checkpoints (``bo_loop.py:281-290``,
     ``data_catalog.py:317-348``) for a state built here, in the raw GPyTorch parametrisation that
     ``from_state_dict(..., noise_constraint="raw")`` reads back: ``Positive`` (softplus) lengthscales and
-    outputscale, the BO loop's ``GreaterThan(..., transform=None)`` noise (``factory.py:95-104``: raw =
-    noise), ``mean_module.raw_constant``, and BoTorch's ``Standardize(m=1)`` buffers when the output is
-    standardised.  ``from_state_dict(to_state_dict(m), train_x, train_y_problem_units, ...)`` rebuilds ``m``
-    (hyperparameters to the last ulp of softplus∘inv_softplus)."""
+    outputscale, the BO loop's ``GreaterThan(min_noise_se**2, transform=None)`` noise (``factory.py:95-104``:
+    raw = noise; lower bound ``MIN_NOISE_SE_FIXED**2`` on the ``never`` path, ``MIN_NOISE_SE**2`` otherwise,
+    ``factory.py:41-43``), ``mean_module.raw_constant``, BoTorch's ``Standardize(m=1)`` buffers when the output
+    is standardised, and the ``LikelihoodList`` copies ``likelihood.likelihoods.i.*`` every ``ModelListGP``
+    holds (the keys of the reference's own ``data/shared/gp-problem`` state dicts, tests/golden/ref_schema.json).
+
+    ``model_config`` (the reference's ``model`` config section, ``bo_smoke.reference_model_config``): the
+    surrogate ``build_mll_and_model`` builds from it also carries its priors' buffers
+    (``<module>.<name>_prior.concentration`` / ``.rate``, ``factory.py:91-151``); without it the never-path
+    floor and no priors are assumed.  The prior buffer names follow gpytorch 1.11's ``GammaPrior``, which is
+    not importable here: that part of the key set is unpinned.
+    ``from_state_dict(to_state_dict(m), train_x, train_y_problem_units, ...)`` rebuilds ``m`` (hyperparameters
+    to the last ulp of softplus∘inv_softplus)."""
     sd: Dict[str, torch.Tensor] = {}
     f64 = dict(dtype=torch.double)
+    fit = (model_config or {}).get("fit_hyperparams", "never")
+    floor = (MIN_NOISE_SE_FIXED if fit == "never" else MIN_NOISE_SE) ** 2
+    outs_cfg = (model_config or {}).get("outputs") or [None] * model.num_outputs
+    if len(outs_cfg) != model.num_outputs:
+        raise ValueError(f"model_config has {len(outs_cfg)} outputs for a {model.num_outputs}-output model")
+    lik_list: Dict[str, torch.Tensor] = {}
     for i, st in enumerate(model.models):
         p = f"models.{i}."
-        sd[p + "likelihood.noise_covar.raw_noise"] = torch.tensor([st.noise], **f64)
-        sd[p + "likelihood.noise_covar.raw_noise_constraint.lower_bound"] = torch.tensor(0.0, **f64)
-        sd[p + "likelihood.noise_covar.raw_noise_constraint.upper_bound"] = torch.tensor(float("inf"), **f64)
+        cfg = outs_cfg[i] or {}
+        lik = {"noise_covar.raw_noise": torch.tensor([st.noise], **f64),
+               "noise_covar.raw_noise_constraint.lower_bound": torch.tensor(floor, **f64),
+               "noise_covar.raw_noise_constraint.upper_bound": torch.tensor(float("inf"), **f64)}
+        for k, v in _prior_buffers((cfg.get("likelihood") or {}).get("noise_prior")).items():
+            lik["noise_covar.noise_prior." + k] = torch.tensor(v, **f64)
+        for k, v in lik.items():
+            sd[p + "likelihood." + k] = v
+            lik_list[f"likelihood.likelihoods.{i}." + k] = v.clone()
         sd[p + "mean_module.raw_constant"] = torch.tensor(float(st.mean_constant), **f64)
         sd[p + "covar_module.raw_outputscale"] = _inv_softplus(torch.tensor(float(st.outputscale), **f64))
         sd[p + "covar_module.base_kernel.raw_lengthscale"] = _inv_softplus(
@@ -232,8 +268,13 @@ def to_state_dict(model: ModelListGPState) -> Dict[str, torch.Tensor]:
         for k in ("covar_module.raw_outputscale_constraint", "covar_module.base_kernel.raw_lengthscale_constraint"):
             sd[p + k + ".lower_bound"] = torch.tensor(0.0, **f64)
             sd[p + k + ".upper_bound"] = torch.tensor(float("inf"), **f64)
+        kcfg = cfg.get("kernel") or {}
+        for name, mod in (("lengthscale_prior", "covar_module.base_kernel."), ("outputscale_prior", "covar_module.")):
+            for k, v in _prior_buffers(kcfg.get(name)).items():
+                sd[p + mod + name + "." + k] = torch.tensor(v, **f64)
         if st.y_mean != 0.0 or st.y_std != 1.0:
             sd[p + "outcome_transform.means"] = torch.tensor([[st.y_mean]], **f64)
             sd[p + "outcome_transform.stdvs"] = torch.tensor([[st.y_std]], **f64)
             sd[p + "outcome_transform._stdvs_sq"] = torch.tensor([[st.y_std ** 2]], **f64)
+    sd.update(lik_list)
     return sd

@@ -44,8 +44,9 @@ def draw_sobol_samples(bounds: Tensor, n: int, q: int, seed: Optional[int] = Non
     d = lower.shape[-1]
     if seed is None:
         seed = int(torch.randint(0, 10**6, (1,)).item())
-    eng = torch.quasirandom.SobolEngine(d * q, scramble=True, seed=seed)
-    raw = eng.draw(n, dtype=lower.dtype).to(lower.device).view(n, q, d)
+    from .utils import sobol_draw
+
+    raw = sobol_draw(d * q, n, seed, lower.dtype).to(lower.device).view(n, q, d)
     return lower + (upper - lower) * raw
 
 
@@ -177,7 +178,8 @@ class DiscreteKgOptimisationSpec:
     """
 
     def __init__(self, n_discretisation_points_per_axis: int, num_restarts: int, raw_samples: int,
-                 batch_limit: int, max_iter: int, device=None, seed: Optional[int] = None):
+                 batch_limit: int, max_iter: int, device=None, seed: Optional[int] = None,
+                 acq_factory: Optional[Callable] = None):
         self.n_discretisation_points_per_axis = n_discretisation_points_per_axis
         self.num_restarts = num_restarts
         self.raw_samples = raw_samples
@@ -185,6 +187,9 @@ class DiscreteKgOptimisationSpec:
         self.max_iter = max_iter
         self.device = device
         self.seed = seed
+        # acq_factory(model, x_discretisation, scalarisation_weights, target_output_ix) -> acquisition:
+        # None builds the device DiscreteKnowledgeGradient (tests inject the oracle's KG to compare runs)
+        self.acq_factory = acq_factory
 
     def _options(self) -> Dict:
         opts = {"batch_limit": self.batch_limit, "maxiter": self.max_iter}
@@ -197,6 +202,8 @@ class DiscreteKgOptimisationSpec:
         from .utils import make_torch_std_grid
 
         disc = make_torch_std_grid(self.n_discretisation_points_per_axis, input_dim, {"dtype": torch.double})
+        if self.acq_factory is not None:
+            return self.acq_factory(model, disc, scalarisation_weights, target)
         return DiscreteKnowledgeGradient(model, x_discretisation=disc, scalarisation_weights=scalarisation_weights,
                                          target_output_ix=target, device=self.device)
 

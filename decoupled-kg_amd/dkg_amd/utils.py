@@ -29,14 +29,27 @@ def is_power_of_2(n) -> bool:
     return n != 0 and (n & (n - 1)) == 0
 
 
+def sobol_draw(dim: int, n: int, seed=None, dtype=torch.double) -> torch.Tensor:
+    """``n`` scrambled Sobol points in [0, 1)^dim of ``dtype``.  torch's ``SobolEngine`` computes its first
+    point in the *default* dtype when it is constructed, so under a float32 default the first point would be
+    rounded to float32 whatever ``draw``'s dtype; the reference runs with a float64 default
+    (``pipeline/main.py:223``), so the engine is built under ``dtype`` here."""
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        eng = torch.quasirandom.SobolEngine(dim, scramble=True, seed=seed)
+        return eng.draw(n, dtype=dtype)
+    finally:
+        torch.set_default_dtype(prev)
+
+
 def sample_simplex(d: int, n: int = 1, qmc: bool = False, seed=None, device=None,
                    dtype=torch.double) -> torch.Tensor:
     """Uniform samples on the (d-1)-simplex via sorted uniforms (BoTorch)."""
     if d == 1:
         return torch.ones(n, 1, device=device, dtype=dtype)
     if qmc:
-        eng = torch.quasirandom.SobolEngine(d - 1, scramble=True, seed=seed)
-        u = eng.draw(n, dtype=dtype)
+        u = sobol_draw(d - 1, n, seed, dtype)
     else:
         g = torch.Generator()
         if seed is not None:

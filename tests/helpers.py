@@ -29,6 +29,33 @@ def stated_tol(ref: torch.Tensor, amax: torch.Tensor, rtol: float = 1e-6) -> tor
     return rtol * ref.abs() + 64.0 * EPS * amax
 
 
+def grad_scale(om, X, D, W, target=None, h: float = 1e-6) -> torch.Tensor:
+    """Per candidate, the magnitude G of the terms dKG/dx sums: with the envelope fixed,
+    dKG_w/dx = sum_e [dPhi_e da_e/dx - dphi_e db_e/dx] - [line 0 attains max a] da_0/dx, where only line 0's
+    intercept and the slopes depend on x, so every term is bounded by
+    G = |da_0/dx|_inf + max_k |db_k/dx|_inf (max over the scalarisations).  Central differences of the
+    oracle's lines (a magnitude for the tolerance, not a parity value)."""
+    from oracle.discretekg import lines_batched
+
+    B, d = X.shape
+    G = torch.zeros(B, dtype=torch.double)
+    for j in range(d):
+        e = torch.zeros_like(X)
+        e[:, j] = h
+        ap, bp = lines_batched(om, X + e, D, W, target)
+        am, bm = lines_batched(om, X - e, D, W, target)
+        da0 = ((ap[..., 0] - am[..., 0]) / (2 * h)).abs()             # [B, S]
+        db = ((bp - bm) / (2 * h)).abs().amax(-1)                      # [B, S]
+        G = torch.maximum(G, (da0 + db).amax(-1))
+    return G
+
+
+def grad_tol(g_ref: torch.Tensor, G: torch.Tensor, rtol: float = 1e-6) -> torch.Tensor:
+    """The gradient's tolerance, stated like the KG's: 1e-6 |g| + 64 eps G per coordinate, G the magnitude of
+    the terms the gradient sums (grad_scale): the fp64 cancellation floor of that sum."""
+    return rtol * g_ref.abs() + 64.0 * EPS * G.reshape(-1, 1)
+
+
 SQRT_2_OVER_PI = math.sqrt(2.0 / math.pi)
 
 
@@ -75,8 +102,8 @@ def parity_case(state, D, W, X, target, dev="cuda"):
       lines   : device lines (dkg_plan_lines, the envelope's own) vs oracle.lines_batched;
       envelope: device KG per pair vs the reference walk + expectation on the *same* (device) lines,
                 stated tolerance (1e-6 |KG| + 64 eps max|a|) -- isolates the envelope kernel;
-      kg      : device KG vs oracle KG per candidate, stated tolerance plus kg_line_floor of the
-                measured line gap (the posterior stage's rounding, propagated by the Lipschitz bound).
+      kg      : device KG vs oracle KG per candidate at the stated tolerance alone; the line gap's
+                Lipschitz bound (kg_line_floor) is reported as a diagnostic only (``kg_ratio``).
     """
     from dkg_amd import DiscreteKnowledgeGradient
     from oracle.discretekg import kg_pairs_from_lines, lines_batched
@@ -96,15 +123,17 @@ def parity_case(state, D, W, X, target, dev="cuda"):
     amax = amax_pair.amax(-1)                              # [B]
     da, db = line_gap(a_dev, b_dev, a_ref, b_ref)
     tol_env = stated_tol(pairs_same_lines, a_dev.abs().amax(-1))
-    tol_kg = stated_tol(kg_ref, amax) + kg_line_floor(da, db)
+    tol_kg = stated_tol(kg_ref, amax)
     err_kg = (kg - kg_ref).abs()
     return {
         "B": X.shape[0], "S": W.shape[0], "lines": a_dev.shape[-1],
         "line_rel_a": float(da.max() / a_ref.abs().max().clamp_min(1e-300)),
         "line_rel_b": float(db.max() / b_ref.abs().max().clamp_min(1e-300)),
         "envelope_ratio": float(((pairs - pairs_same_lines).abs() / tol_env).max()),
-        "kg_ratio": float((err_kg / tol_kg).max()),
-        "kg_ratio_stated_only": float((err_kg / stated_tol(kg_ref, amax)).max()),
+        # the asserted ratio (stated tolerance alone), and the same error against the stated tolerance plus
+        # the line gap's Lipschitz bound (diagnostic: how much of the tolerance the line gap alone could use)
+        "kg_ratio_stated_only": float((err_kg / tol_kg).max()),
+        "kg_ratio": float((err_kg / (tol_kg + kg_line_floor(da, db))).max()),
         "kg_max_abs_err": float(err_kg.max()),
         "kg_ref_max": float(kg_ref.abs().max()),
         "line_floor_max": float(kg_line_floor(da, db).max()),
@@ -120,7 +149,9 @@ def check_parity_case(res):
         f"device lines vs oracle: rel {res['line_rel_a']:.3e} / {res['line_rel_b']:.3e} > {LINE_RTOL}")
     kg, kg_ref, tol_kg, pairs, pairs_same, tol_env = res["_tensors"]
     assert_within(pairs, pairs_same, tol_env, "envelope on identical lines")
-    assert_within(kg, kg_ref, tol_kg, "end-to-end KG")
+    assert_within(kg, kg_ref, tol_kg, "end-to-end KG (stated tolerance)")
+    print(f"parity: KG err/stated tol {res['kg_ratio_stated_only']:.3g}, line-gap floor max "
+          f"{res['line_floor_max']:.3g} (diagnostic, not asserted)")
 
 
 def load_golden(name: str):

@@ -136,3 +136,49 @@ def test_reads_the_reference_shared_gp_problem():
     assert {"bounds", "fixed_hyperparams", "model_state_dict", "train_x", "train_y"} <= set(prob)
     m = from_state_dict(prob["model_state_dict"], prob["train_x"], prob["train_y"], bounds=None)
     assert m.num_outputs == len(prob["bounds"]) or m.num_outputs >= 1
+
+
+SCHEMA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_schema.json")
+
+
+def test_checkpoint_model_config_is_the_reference_schema():
+    """The SMOKE loop's checkpoint config is the reference's ``model`` section of
+    config/experiment-lengthscales.yaml as cli.py:22-37 completes it for --fit-hyperparams never (the fixture
+    tests/golden/ref_schema.json, made by make_ref_schema.py): what build_mll_and_model reads."""
+    import copy
+    import json
+
+    from dkg_amd.bo_smoke import reference_model_config
+
+    ref = copy.deepcopy(json.load(open(SCHEMA))["model"])
+    ref["fit_hyperparams"] = "never"
+    for o in ref["outputs"]:
+        o["standardize_output"] = False
+    assert reference_model_config(2, torch.tensor([[0.0, 0.0], [1.0, 1.0]])) == ref
+
+
+def test_checkpoint_state_dict_has_the_reference_key_set():
+    """Every key (and shape) of a reference-built ModelListGP state dict (the reference's own GP-problem
+    fixture) is in the checkpointed state dict, with the never-path noise floor as the constraint's lower
+    bound (factory.py:41-43, 95-104); the only extra keys are the config's Gamma priors' buffers."""
+    import json
+
+    from dkg_amd.bo_smoke import reference_model_config
+
+    ref = json.load(open(SCHEMA))["state_dict_keys"]
+    g = torch.Generator().manual_seed(4)
+    m = ModelListGPState(*[SingleTaskGPState(torch.rand(6, 2, generator=g, dtype=torch.double),
+                                             torch.randn(6, generator=g, dtype=torch.double),
+                                             torch.tensor([0.2, 1.8], dtype=torch.double), 1.0, 1e-8, 0.0)
+                           for _ in range(2)])
+    sd = to_state_dict(m, reference_model_config(2, torch.tensor([[0.0, 0.0], [1.0, 1.0]])))
+    for k, shape in ref.items():
+        assert k in sd, k
+        assert list(sd[k].shape) == shape, k
+    assert all("_prior." in k for k in set(sd) - set(ref))
+    assert float(sd["models.0.likelihood.noise_covar.raw_noise_constraint.lower_bound"]) == 1e-8
+    assert float(sd["likelihood.likelihoods.1.noise_covar.raw_noise"]) == 1e-8
+    assert float(sd["models.0.covar_module.base_kernel.lengthscale_prior.rate"]) == 10.0
+    m2 = from_state_dict(sd, [st.train_x for st in m.models], [st.train_y for st in m.models],
+                         noise_constraint="raw")
+    assert [st.noise for st in m2.models] == [1e-8, 1e-8]

@@ -79,6 +79,20 @@ def test_sharded_matches_unsharded(tmp_path, axis, B, S, target):
         # the gradient floor of tests/test_gpu_grad.py: 1e-9 of the largest component (cancellation in E - max a)
         torch.testing.assert_close(g, g_ref, rtol=1e-9, atol=1e-9 * float(g_ref.abs().max()))
     assert torch.equal(res["grads"][0], res["grads"][1])
+    assert torch.equal(res["kg_async"], res["kg"])
+    assert_within(res["kg_async_flip"], ref.flip(0), stated_tol(ref.flip(0), amax.flip(0)))
+
+
+def test_idle_rank_zeros_keep_nonfinite_inputs_out():
+    """A rank with no local work joins the backward through zeros connected to X: an inf / NaN coordinate in X
+    gives an exact zero gradient there, not NaN (which the all-reduce would spread to every candidate)."""
+    from dkg_amd.dist import _zeros_like_graph
+
+    x = torch.tensor([[0.5, float("inf")], [float("nan"), 0.1]], dtype=torch.double, requires_grad=True)
+    z = _zeros_like_graph(x, 3, torch.device("cpu"))
+    assert torch.equal(z, torch.zeros(3, dtype=torch.double)) and z.requires_grad
+    (z * torch.tensor([1.0, 2.0, 3.0], dtype=torch.double)).sum().backward()
+    assert torch.equal(x.grad, torch.zeros_like(x))
 
 
 @pytest.mark.parametrize("mode,steps,every", [("gather", 7, 3), ("gather", 6, 3), ("reduce", 7, 3),

@@ -3,15 +3,13 @@
 CPU: the oracle still reproduces the committed vectors (guards the restatement
 against drift) and its batched form agrees with its per-candidate form.
 GPU: the HIP path through the C ABI matches them within the stated tolerance
-(1e-6 |KG| + 64 eps max|a|, plus the measured device-vs-oracle line gap propagated
-by helpers.kg_line_floor; tests/helpers.py).
+(1e-6 |KG| + 64 eps max|a|, tests/helpers.py), nothing added.
 """
 
 import pytest
 import torch
 
-from helpers import (assert_within, check_parity_case, kg_line_floor, line_gap, load_golden, parity_case,
-                     stated_tol)
+from helpers import assert_within, check_parity_case, load_golden, parity_case, stated_tol
 from oracle.discretekg import (calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output,
                                discrete_kg_batched, kg_pairs_from_lines, lines_batched)
 
@@ -61,11 +59,9 @@ def test_native_matches_golden(name, key, target):
     kg = acq(X.unsqueeze(-2).cuda()).cpu()
     res = parity_case(state, D, W, X, target)
     check_parity_case(res)
-    a_dev, b_dev = acq._plan_for(X.shape[0]).lines(X.cuda())
-    a_ref, b_ref = lines_batched(om, X, D, W, target)
-    da, db = line_gap(a_dev, b_dev, a_ref, b_ref)
+    a_ref, _ = lines_batched(om, X, D, W, target)
     ref = t[f"kg_{key}"]
-    assert_within(kg, ref, stated_tol(ref, a_ref.abs().amax((-1, -2))) + kg_line_floor(da, db))
+    assert_within(kg, ref, stated_tol(ref, a_ref.abs().amax((-1, -2))), "KG vs golden (stated tolerance)")
 
 
 @pytest.mark.gpu

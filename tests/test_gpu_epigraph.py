@@ -238,6 +238,46 @@ def test_epigraph_batched_matches_single():
         assert torch.equal(idx[p, :m].cpu(), ri) and torch.equal(xs[p, : m - 1].cpu(), rx)
 
 
+def test_epigraph_far_breakpoints_redo_and_padding():
+    """Envelope breakpoints near 1e10 and 1e11 (two nearly parallel lines on the hull): the first list walk
+    leaves the 2^30 guard and is redone over a list filtered at the wider margin that covers it; the result
+    is the reference walk, and every index / intersection past the count is -1 / NaN."""
+    from dkg_amd import calculate_epigraph_indices_batched
+
+    g = torch.Generator().manual_seed(11)
+    a = torch.cat([torch.tensor([-5.0, 1.0, 1.0 - 1e-3, -1e11], dtype=torch.double),
+                   -10.0 - torch.rand(60, generator=g, dtype=torch.double)])
+    b = torch.cat([torch.tensor([-2.0, 0.0, 1e-13, 1.0], dtype=torch.double),
+                   2.0 * torch.rand(60, generator=g, dtype=torch.double) - 1.0])
+    assert _assert_same_walk(a, b) >= 3
+    A, Bm = torch.stack([a, a.flip(0)]), torch.stack([b, b.flip(0)])
+    idx, xs, cnt = calculate_epigraph_indices_batched(A.to(DEV), Bm.to(DEV))
+    idx, xs, cnt = idx.cpu(), xs.cpu(), cnt.cpu()
+    for p in range(2):
+        ri, rx = ref_epigraph(A[p], Bm[p])
+        m = int(cnt[p])
+        assert m == len(ri) and torch.equal(idx[p, :m], ri) and torch.equal(xs[p, : m - 1], rx)
+        assert bool((idx[p, m:] == -1).all()) and bool(xs[p, m - 1:].isnan().all())
+        assert float(rx.abs().max()) > 2.0 ** 30
+
+
+def test_epigraph_padding_past_the_count():
+    """Every set of a random batch: indices past the count are -1 and intersections past count - 1 NaN."""
+    from dkg_amd import calculate_epigraph_indices_batched
+
+    g = torch.Generator().manual_seed(12)
+    for L in (5, 200, 1025, 3000):
+        a = torch.randn(16, L, generator=g, dtype=torch.double)
+        b = torch.randn(16, L, generator=g, dtype=torch.double)
+        b[:2] = 0.0  # short-circuit sets: one index, no intersection
+        idx, xs, cnt = calculate_epigraph_indices_batched(a.to(DEV), b.to(DEV))
+        idx, xs, cnt = idx.cpu(), xs.cpu(), cnt.cpu()
+        for p in range(16):
+            m = int(cnt[p])
+            assert bool((idx[p, m:] == -1).all()) and bool((idx[p, :m] >= 0).all())
+            assert bool(xs[p, max(m - 1, 0):].isnan().all()) and not bool(xs[p, : max(m - 1, 0)].isnan().any())
+
+
 # ---------------------------------------------------------------- the forward's own lines
 def _plan_lines(workload, nX, target):
     from dkg_amd import DiscreteKnowledgeGradient

@@ -5,9 +5,10 @@ gradcheck on it; optimize_acqf's L-BFGS-B needs dKG/dX).  The oracle is the
 structure-faithful restatement; torch.autograd through it is the gradient
 reference (its own gradcheck passes in test_oracle_kats.py).
 
-Tolerance: |g - g_ref| <= 1e-6 |g_ref| + 1e-9 * max|g_ref| over the batch,
-per coordinate (the absolute term is the rounding floor of the envelope sums
-relative to the largest gradient in the batch).
+Tolerance, stated like the KG's (tests/helpers.grad_tol): per candidate and coordinate
+|g - g_ref| <= 1e-6 |g_ref| + 64 eps G, with G = |da_0/dx| + max_k |db_k/dx| the magnitude of the terms
+the gradient sums (helpers.grad_scale): the fp64 cancellation floor of that sum, as 64 eps max|a| is
+KG's.  Measured worst ratio 0.072 at the headline, 0.0011 on headline_nd (profiles/r03/grad_probe.json).
 """
 
 import pytest
@@ -15,8 +16,8 @@ import torch
 
 from dkg_amd import DiscreteKnowledgeGradient
 from dkg_amd.synthetic import WORKLOADS, make_problem
-from helpers import load_golden, to_oracle
-from oracle.discretekg import discrete_kg_batched
+from helpers import assert_within, grad_scale, grad_tol, load_golden, stated_tol, to_oracle
+from oracle.discretekg import discrete_kg_batched, lines_batched
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -37,11 +38,13 @@ def native_grad(state, X, D, W, target):
     return kg.detach().cpu(), g.cpu()
 
 
-def assert_grad_close(g, ref):
-    floor = 1e-9 * ref.abs().max().clamp_min(1e-300)
+def assert_grad_close(g, ref, G):
+    """|g - ref| <= 1e-6 |ref| + 64 eps G per candidate (G from helpers.grad_scale); returns the worst ratio."""
     err = (g - ref).abs()
-    tol = 1e-6 * ref.abs() + floor
-    assert bool((err <= tol).all()), f"max err {err.max():.3e}, worst ratio {(err / tol).max():.3f}"
+    tol = grad_tol(ref, G)
+    ratio = err / tol
+    assert bool((err <= tol).all()), f"max err {err.max():.3e}, worst err/tol {ratio.max():.3f}"
+    return float(ratio.max())
 
 
 @pytest.mark.parametrize("workload", ["small", "parity6d"])
@@ -54,7 +57,7 @@ def test_grad_vs_oracle(workload, target):
     kg_ref, g_ref = oracle_grad(om, X, D, W, target)
     kg, g = native_grad(model, X, D, W, target)
     assert g.shape == X.shape
-    assert_grad_close(g, g_ref)
+    assert_grad_close(g, g_ref, grad_scale(om, X, D, W, target))
 
 
 @pytest.mark.parametrize("name", ["lengthscales0", "observationnoise0"])
@@ -64,7 +67,7 @@ def test_grad_golden_problems(name, target):
     X = X[:10]
     _, g_ref = oracle_grad(om, X, D, W, target)
     _, g = native_grad(state, X, D, W, target)
-    assert_grad_close(g, g_ref)
+    assert_grad_close(g, g_ref, grad_scale(om, X, D, W, target))
 
 
 def test_grad_matches_central_differences():
@@ -85,16 +88,20 @@ def test_grad_matches_central_differences():
     torch.testing.assert_close(g.cpu(), fd, rtol=1e-4, atol=1e-7 * fd.abs().max().item())
 
 
+@pytest.mark.parametrize("workload", ["headline", "headline_nd"])
 @pytest.mark.parametrize("target", [None, 1])
-def test_grad_vs_oracle_headline(target):
-    """Headline workload (n 256, N 1024, S 16): dKG/dx against the oracle's autograd, 32 candidates."""
-    w = WORKLOADS["headline"]
+def test_grad_vs_oracle_headline_all_candidates(workload, target):
+    """Headline sizes (n 256, N 1024, S 16), every one of the 128 candidates: dKG/dx against the oracle's
+    autograd.  headline_nd (d = 6) has KG > 0 on every pair, so every gradient there is a walked envelope's."""
+    w = WORKLOADS[workload]
     model, D, X, W = make_problem(w)
-    X = X[:32]
     om = to_oracle(model)
-    _, g_ref = oracle_grad(om, X, D, W, target)
+    kg_ref, g_ref = oracle_grad(om, X, D, W, target)
     _, g = native_grad(model, X, D, W, target)
-    assert_grad_close(g, g_ref)
+    assert g.shape == X.shape == (128, w.d)
+    if workload == "headline_nd":
+        assert int((kg_ref > 0).sum()) >= 120
+    print(f"{workload} target={target}: worst err/tol {assert_grad_close(g, g_ref, grad_scale(om, X, D, W, target)):.3g}")
 
 
 def test_grad_headline_batch_consistent():
@@ -169,10 +176,10 @@ def test_overflow_walk_path_value_and_grad(workload, target):
     plan_grad = acq._state.plan(acq._W, target, 16, grad=True, force_walk=True)
     kg2, g = plan_grad.forward_grad(Xd)
     assert tgt == plan_fwd.target
-    scale = kg_ref.abs().max().item()
-    assert (kg - kg_ref).abs().max().item() <= 1e-6 * scale + 1e-15
-    assert (kg2.cpu() - kg_ref).abs().max().item() <= 1e-6 * scale + 1e-15
-    assert_grad_close(g.cpu(), g_ref)
+    amax = lines_batched(om, X, D, W, target)[0].abs().amax((-1, -2))
+    assert_within(kg, kg_ref, stated_tol(kg_ref, amax), "force-walk KG")
+    assert_within(kg2.cpu(), kg_ref, stated_tol(kg_ref, amax), "force-walk KG (gradient plan)")
+    assert_grad_close(g.cpu(), g_ref, grad_scale(om, X, D, W, target))
 
 
 @pytest.mark.parametrize("target", [None, 1])
@@ -189,7 +196,7 @@ def test_flat_early_out_matches_the_full_gradient_path(target):
     full = acq._state.plan(acq._W, acq._target, X.shape[0], grad=True, force_walk=True)
     kg_f, g_f = full.forward_grad(Xd)
     torch.testing.assert_close(kg, kg_f, rtol=1e-12, atol=0.0)
-    assert_grad_close(g.cpu(), g_f.cpu())
+    assert_grad_close(g.cpu(), g_f.cpu(), grad_scale(to_oracle(model), X, D, W, target))
     # off the discretisation, KG = 0 leaves at most denormal-scale gradient terms (breakpoints at 37-40
     # standard deviations, where psi rounds to 0 before phi does) on either path
     zero = kg_f == 0

@@ -2,11 +2,11 @@
 
 Every check goes through the C ABI (``include/dkg.h``) via ``dkg_amd``.
 Tolerance (BASELINE.md "Accuracy"): |KG_gpu - KG_oracle| <= 1e-6 |KG_oracle|
-+ 64 eps max|a|.  End to end the lines themselves come out of two fp64 builds of an ill-conditioned
-posterior, so there the bound adds the measured line gap propagated by KG's Lipschitz constants
-(helpers.kg_line_floor: 2 max|da| + sqrt(2/pi) max|db|), and the line gap itself must stay within
-helpers.LINE_RTOL; the envelope kernel alone is held to the stated tolerance on identical lines
-(helpers.parity_case).  Worst ratios: profiles/r02_parity.json (tools/parity_report.py).
++ 64 eps max|a|, asserted as stated, end to end and on every candidate.  The device lines must also
+stay within helpers.LINE_RTOL of the oracle's, and the envelope kernel alone is held to the stated
+tolerance on identical lines (helpers.parity_case).  The line gap's Lipschitz bound
+(helpers.kg_line_floor) is printed as a diagnostic only.  Worst ratios: profiles/r03_parity.json
+(tools/parity_report.py).
 """
 
 import math
@@ -14,13 +14,11 @@ import math
 import pytest
 import torch
 
-from helpers import (EPS, assert_within, check_parity_case, kg_line_floor, line_gap, parity_case,
-                     stated_tol, to_oracle, to_state)
+from helpers import assert_within, check_parity_case, parity_case, stated_tol, to_oracle, to_state
 from oracle.discretekg import (
     _kg_from_lines,
     calculate_discrete_kg,
     calculate_discrete_kg_conditioning_on_single_output,
-    discrete_kg_batched,
     discrete_kg_forward,
     lines_batched,
 )
@@ -200,8 +198,7 @@ def test_reference_kat_scalars(ref_model):
 @pytest.mark.parametrize("workload", ["small", "parity6d"])
 @pytest.mark.parametrize("target", [None, 0, 1])
 def test_forward_vs_faithful_oracle(workload, target):
-    """The per-candidate, dense-covariance oracle (the reference's structure); tolerance: stated +
-    the line-gap floor measured against the batched oracle's lines (same math, other summation order)."""
+    """The per-candidate, dense-covariance oracle (the reference's structure), stated tolerance alone."""
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
@@ -211,10 +208,8 @@ def test_forward_vs_faithful_oracle(workload, target):
     got = acq(X.unsqueeze(-2))
     om = to_oracle(model)
     ref = discrete_kg_forward(om, X.unsqueeze(-2), D, W, target)
-    a_dev, b_dev = acq._plan_for(16).lines(X.to(DEV))
-    a_ref, b_ref = lines_batched(om, X, D, W, target)
-    da, db = line_gap(a_dev, b_dev, a_ref, b_ref)
-    assert_within(got, ref, stated_tol(ref, a_ref.abs().amax((-1, -2))) + kg_line_floor(da, db))
+    a_ref, _ = lines_batched(om, X, D, W, target)
+    assert_within(got, ref, stated_tol(ref, a_ref.abs().amax((-1, -2))), "KG vs faithful oracle (stated tolerance)")
     assert bool((got >= 0).all())
 
 
@@ -339,12 +334,18 @@ def test_wave_butterfly_primitives():
 # ---------------------------------------------------------------- stress sizes
 @pytest.mark.parametrize("target", [None, 2])
 def test_stress_config_parity(target):
-    """BASELINE.json configs[4] shape (m=3, n=1024, N=4096 = 64^2 grid, S=32), fp64:
-    the envelope streams its 4097 lines per pair from global memory."""
+    """BASELINE.json configs[4] shape (m=3, n=1024, N=4096 = 64^2 grid, S=32), fp64, 64 candidates: the 48
+    with the largest device KG (KG > 0: walked envelopes) and the 16 smallest; stated tolerance on every one.
+    Measured worst KG err/tol 0.042 (full) / 0.061 (target 2) (profiles/r03/grad_probe.json)."""
+    from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
     model, D, X, W = make_problem(WORKLOADS["stress"])
-    check_parity_case(parity_case(model, D, W, X[:4], target))
+    kg = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)(X.to(DEV).unsqueeze(-2)).cpu()
+    order = torch.argsort(kg, descending=True)
+    pick = torch.cat([order[:48], order[-16:]])
+    assert int((kg[pick] > 0).sum()) >= 48
+    check_parity_case(parity_case(model, D, W, X[pick], target))
 
 
 @pytest.mark.parametrize("target", [None, 1])
