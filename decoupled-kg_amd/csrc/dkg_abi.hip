@@ -34,6 +34,7 @@ int hip_check(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct WsLayout {
+  size_t sync_bytes;  // the fused forward's counter block, at offset 0 (zeroed by one memset)
   size_t jq[DKG_MAX_OUTPUTS];
   size_t gmu[DKG_MAX_OUTPUTS];
   size_t qxrm[DKG_MAX_OUTPUTS];
@@ -51,8 +52,11 @@ struct WsLayout {
 
 WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, int flags = 0) {
   WsLayout L{};
-  size_t off = 0;
   const size_t Bp = pad16(std::max(B, 1));
+  // fused hand-off counters, one per 128-byte line: cnt1 [m][Bp / 16], cnt2 [ceil(B / 32)], done; then the err word
+  L.sync_bytes = ((((size_t)m * (Bp / 16) + (Bp + 31) / 32 + 1) * HANDOFF_STRIDE * sizeof(unsigned long long) +
+                   sizeof(int)) + 15) & ~(size_t)15;
+  size_t off = align256(L.sync_bytes);
   for (int i = 0; i < m; ++i) {
     if (flags & DKG_PLAN_GRAD) {
       L.jq[i] = off;
@@ -145,7 +149,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
-  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK | DKG_PLAN_F32))
+  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK | DKG_PLAN_F32 | DKG_PLAN_FUSED))
     return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
   if (want_grad && (flags & DKG_PLAN_F32))
     return fail(DKG_ERR_UNSUPPORTED, "the fp32 plan (DKG_PLAN_F32) is forward only; the gradient runs in fp64");
@@ -204,6 +208,22 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
   static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
   P->debug_stamp = dst ? std::atoi(dst) : 0;
+  // the fused one-launch forward (dkg_fused.h) on request (DKG_PLAN_FUSED, or DKG_FUSED=1 in the
+  // environment for A/B runs): fp64, staged lines, no test hooks
+  static const char* fused_env = std::getenv("DKG_FUSED");
+  const bool split_stages = !((flags & DKG_PLAN_FUSED) || (fused_env && std::atoi(fused_env))) ||
+                            (flags & DKG_PLAN_FORCE_WALK);
+  P->sync = reinterpret_cast<unsigned long long*>(ws);
+  P->sync_bytes = L.sync_bytes;
+  {
+    const size_t words = ((size_t)m * (pad16(std::max(max_B, 1)) / 16) + (pad16(std::max(max_B, 1)) + 31) / 32 + 1) *
+                         HANDOFF_STRIDE;
+    P->sync_err = reinterpret_cast<int*>(ws + words * sizeof(unsigned long long));
+  }
+  P->fused = (!split_stages && !P->f32 && !P->stream && N >= 1 && N + 1 <= 64 * 17 && !P->debug_env && !P->debug_cov &&
+              !DKG_ABLATIONS && fused_lds_bytes_host(*P) <= 160 * 1024)
+                 ? 1
+                 : 0;
   if (P->debug_stamp) {
     if (!g_kstamps_buf &&
         hip_check(hipMalloc(&g_kstamps_buf, sizeof(unsigned long long) * 3 * KST_WG * 8), "hipMalloc(stamps)"))
@@ -224,7 +244,9 @@ int run_forward(const Plan& h, const Plan* dev, const double* xnew, int B, doubl
   if (stage_ms)
     for (int k = 0; k < 4; ++k)
       if ((st = hip_check(hipEventCreate(&ev[k]), "hipEventCreate"))) return st;
-  if ((st = hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, stream, stage_ms ? ev : nullptr), "forward")))
+  if ((st = hip_check(stage_ms ? launch_forward(h, dev, xnew, B, kg, kg_pairs, stream, ev)
+                                : launch_forward_auto(h, dev, xnew, B, kg, kg_pairs, stream),
+                      "forward")))
     return st;
   if (stage_ms) {
     if ((st = hip_check(hipEventSynchronize(ev[3]), "hipEventSynchronize"))) return st;
@@ -241,6 +263,7 @@ size_t plan_slot_bytes() { return align256(sizeof(Plan)); }
 // covariance row are zeroed here once (the covariance stage writes components
 // < m only), so they enter the line build as 0 with a zero weight.
 int copy_disc_means(const Plan& P, hipStream_t s) {
+  if (int st = hip_check(hipMemsetAsync(P.sync, 0, P.sync_bytes, s), "hipMemsetAsync(sync)")) return st;
   const int rec = cov_rec(P.m);
   if (rec > P.m && P.N > 0) {
     const size_t rows = (size_t)std::max(P.max_B, 1) * P.N;
@@ -397,7 +420,7 @@ size_t dkg_plan_bytes(void) { return sizeof(Plan); }
 int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                         double* kg_pairs, void* stream, int stage, int reps, float* avg_ms) {
   if (!host_plan || !dev_plan || !avg_ms) return fail(DKG_ERR_ARG, "NULL pointer");
-  if (stage < 0 || stage > 2 || reps < 1) return fail(DKG_ERR_ARG, "stage=%d reps=%d", stage, reps);
+  if (stage < 0 || stage > 3 || reps < 1) return fail(DKG_ERR_ARG, "stage=%d reps=%d", stage, reps);
   const Plan& h = *static_cast<const Plan*>(host_plan);
   if (B < 1 || B > h.max_B) return fail(DKG_ERR_ARG, "B=%d outside [1, %d]", B, h.max_B);
   if (!xnew || !kg) return fail(DKG_ERR_ARG, "NULL data pointer");
@@ -411,7 +434,10 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
   if ((st = hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr), "forward"))) return st;
   (void)hipEventRecord(ev[0], s);
   for (int r = 0; r < reps; ++r)
-    if ((st = hip_check(launch_stage(h, dev, xnew, B, kg, kg_pairs, s, stage), "stage"))) return st;
+    if ((st = hip_check(stage == 3 ? launch_forward_auto(h, dev, xnew, B, kg, nullptr, s)
+                                   : launch_stage(h, dev, xnew, B, kg, kg_pairs, s, stage),
+                        "stage")))
+      return st;
   (void)hipEventRecord(ev[1], s);
   if ((st = hip_check(hipEventSynchronize(ev[1]), "hipEventSynchronize"))) return st;
   float ms = 0.f;
@@ -465,6 +491,20 @@ int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const dou
   return hip_check(launch_forward_grad(h, static_cast<const Plan*>(dev_plan), xnew, B, kg, dkg_dx,
                                        (hipStream_t)stream), "forward_grad");
 }
+
+int dkg_plan_status(const void* host_plan, int* err, int reset, void* stream) {
+  if (!host_plan || !err) return fail(DKG_ERR_ARG, "NULL pointer");
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  hipStream_t s = (hipStream_t)stream;
+  int st;
+  if ((st = hip_check(hipMemcpyAsync(err, h.sync_err, sizeof(int), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(err)")) ||
+      (st = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize")))
+    return st;
+  if (reset) return hip_check(hipMemsetAsync(h.sync, 0, h.sync_bytes, s), "hipMemsetAsync(sync)");
+  return DKG_OK;
+}
+
+int dkg_plan_fused(const void* host_plan) { return host_plan ? static_cast<const Plan*>(host_plan)->fused : 0; }
 
 int dkg_plan_hull_sizes(const void* host_plan, int* out, int B, void* stream) {
   if (!host_plan || !out) return fail(DKG_ERR_ARG, "NULL pointer");

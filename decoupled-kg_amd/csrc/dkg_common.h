@@ -392,4 +392,71 @@ __device__ __forceinline__ double psi(double c) {
   return (c < 0.0) ? r + x : r;
 }
 
+// ---------------------------------------------------------------------------
+// In-launch hand-offs (the fused one-launch forward, dkg_fused.h), MI355X_MICROARCH.md
+// "inter-workgroup visibility" / cdna_hip_programming.md Guideline 16, counter form:
+// producers store the handed-off bytes write-through (sc1: no release fence needed), every
+// storing wave drains them (s_waitcnt vmcnt(0)), the workgroup meets, one lane adds to an
+// arrival counter (agent-scope atomic); a consumer polls that counter from one lane
+// (relaxed, agent scope, s_sleep between polls, bounded), takes ONE agent-scope acquire
+// (invalidates its CU's L1), drains it, and the workgroup meets before any load of the
+// bytes.  Counters are zeroed at plan init and re-zeroed by the launch's last workgroup.
+struct Handoff {
+  unsigned long long* cnt1;  // [m][rt]: cross workgroups done per (output, 16-candidate row tile)
+  unsigned long long* cnt2;  // [nrb]: covariance workgroups done per 32-candidate row block
+  unsigned long long* done;  // envelope workgroups done; the last one re-zeroes every counter
+  int* err;                  // bits of the waits that gave up (bounded spins): 0 when all matched
+  int rt, nrb;               // row tiles, row blocks
+  int rb_rows;               // candidates per row block (the covariance stage's)
+  unsigned long long quota1, quota2, quota_done;
+};
+
+// Polls per wait before it gives up (sets its err bit and goes on): each poll is one memory round trip
+// plus an s_sleep, so a wait that never matches ends in well under a second.
+constexpr unsigned HANDOFF_SPIN_LIMIT = 1u << 18;
+// Counters sit one per 128-byte line (16 words apart): hundreds of workgroups poll them at once, and
+// pollers of different counters must not queue on one line (MI355X_MICROARCH.md row "polling-cost").
+constexpr int HANDOFF_STRIDE = 16;
+
+template <bool WT, class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+  if constexpr (WT) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store ... sc1
+  } else {
+    *p = v;
+  }
+}
+
+// Every storing wave drains its write-through stores; the workgroup meets; one lane counts the arrival.
+__device__ __forceinline__ void handoff_publish(unsigned long long* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until the counters cnt[0], cnt[HANDOFF_STRIDE], ... (count of them) each reached `quota`, then one
+// acquire; the workgroup meets after it.  Between polls the lane sleeps longer the longer it has waited
+// (64 to ~1000 cycles), so early-dispatched consumers do not flood the counters' lines.
+__device__ __forceinline__ void handoff_wait(unsigned long long* cnt, int count, unsigned long long quota, int* err,
+                                             int code) {
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < count; ++i) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(cnt + (size_t)i * HANDOFF_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+             quota) {
+        if (++spins > HANDOFF_SPIN_LIMIT) {
+          __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        if (spins < 8) __builtin_amdgcn_s_sleep(1);
+        else if (spins < 64) __builtin_amdgcn_s_sleep(4);
+        else __builtin_amdgcn_s_sleep(16);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 }  // namespace dkg

@@ -1117,25 +1117,26 @@ __host__ __device__ constexpr int env_waves_per_eu(int maxl, int m, bool grad, b
 // accumulated into dkg[b x d]; the extra LDS follows the survivor lists.
 // STREAM: no LDS staging of the line data; every pass rebuilds the lines
 // chunk by chunk (64 * MAXL lines) from global memory (large N).
-template <int MAXL, int M, bool GRAD, bool STREAM>
+// HO (fused one-launch forward, dkg_fused.h): the covariance rows, variances and means are handed
+// off by the workgroups of this launch: mu_D, the weights and the per-output scalars are staged
+// first, then the wait on the candidate's row block (Handoff cnt2), then its rows; the last
+// envelope workgroup to finish re-zeroes the launch's counters.
 // The line data (mu_all, cov_all), the candidate posteriors (var_all, mux_all)
-// and the weights arrive as kernel arguments, so the first DMA issues after a
+// and the weights arrive as arguments, so the first DMA issues after a
 // single kernel-argument load instead of a pointer chase through the plan.
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(MAXL, M, GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
-                                                       double* __restrict__ pairs_out, int dst,
-                                                       const double* __restrict__ xnew, double* __restrict__ dkg,
-                                                       const double* __restrict__ mu_all,
-                                                       const double* __restrict__ cov_all,
-                                                       const double* __restrict__ var_all,
-                                                       const double* __restrict__ mux_all,
-                                                       const double* __restrict__ wts, long long cov_stride,
-                                                       int bpad) {
+template <int MAXL, int M, bool GRAD, bool STREAM, bool HO = false>
+__device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B, double* __restrict__ kg,
+                                              double* __restrict__ pairs_out, int dst,
+                                              const double* __restrict__ xnew, double* __restrict__ dkg,
+                                              const double* __restrict__ mu_all, const double* __restrict__ cov_all,
+                                              const double* __restrict__ var_all,
+                                              const double* __restrict__ mux_all, const double* __restrict__ wts,
+                                              long long cov_stride, int bpad, int b, int g, int G, double* smem,
+                                              unsigned long long* st, const Handoff* ho = nullptr) {
+  static_assert(!HO || (!GRAD && !STREAM), "the fused forward stages its lines (no gradient, no streaming)");
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space)
   __shared__ double s_pp[DKG_MAX_OUTPUTS * 6];
   __shared__ int s_kind[DKG_MAX_OUTPUTS];  // GRAD: covariance family per output
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x;
-  const int g = blockIdx.y;
   const int SW = blockDim.x >> 6;
   const int lane_k = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1146,8 +1147,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   const int target = P->target;
   const bool full = target < 0;
   static_assert(STREAM || MAXL == 2 || MAXL == 8 || MAXL == 17 || MAXL == 33, "slot bucket");
-  unsigned long long* st = kst_slot(dst, P, 2);
-  if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
   KST_BEGIN(st);
 
   // The DMA sources first, in one scalar-load batch: the LDS-DMA intrinsics
@@ -1210,19 +1209,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
     pp[1] = o->y_mean;
     pp[2] = o->noise;
     pp[3] = o->outputscale;
-    pp[4] = var_all[(size_t)threadIdx.x * bpad + b];
-    pp[5] = mux_all[(size_t)threadIdx.x * bpad + b];
+    if constexpr (!HO) {
+      pp[4] = var_all[(size_t)threadIdx.x * bpad + b];
+      pp[5] = mux_all[(size_t)threadIdx.x * bpad + b];
+    }
     if constexpr (GRAD) s_kind[threadIdx.x] = o->kernel;
   }
   const double* wsrc = wts;
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    if (!STREAM && i < m) {
-      if (i == 0) {
-        dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
-        dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
-      }
-    }
+  if constexpr (!STREAM) {
+    dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
+    if constexpr (!HO) dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
   }
   if constexpr (GRAD) {
     // the candidate's q_i and J_i rows (row-major in the workspace) by LDS-DMA with the line data, so
@@ -1241,7 +1237,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   for (int e = threadIdx.x; e < S * m; e += blockDim.x) lw[e] = wsrc[e];
   if (threadIdx.x < m) {
 #pragma unroll
-    for (int q = 0; q < 6; ++q) s_pp[threadIdx.x * 6 + q] = pp[q];
+    for (int q = 0; q < (HO ? 4 : 6); ++q) s_pp[threadIdx.x * 6 + q] = pp[q];
+  }
+  if constexpr (HO) {
+    // the candidate's row block of covariance rows (and, transitively, its cross stage's means) is out
+    handoff_wait(ho->cnt2 + (size_t)(b / ho->rb_rows) * HANDOFF_STRIDE, 1, ho->quota2, ho->err, 2);
+    if (threadIdx.x < m) {
+      s_pp[threadIdx.x * 6 + 4] = var_all[(size_t)threadIdx.x * bpad + b];
+      s_pp[threadIdx.x * 6 + 5] = mux_all[(size_t)threadIdx.x * bpad + b];
+    }
+    dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
   }
   if constexpr (GRAD) {
     // d mu_i/dx, 1/lengthscale and x_b into registers: per-output pointers by scalar loads (lgkmcnt,
@@ -1767,7 +1772,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int q = 0; q < j1 - j0; ++q) s += skg[q];
-    const int G = gridDim.y;
     if (G == 1) {
       kg[b] = s / (double)S;
     } else if (G == 2) {
@@ -1789,8 +1793,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
       }
     }
   }
+  if constexpr (HO) {
+    // launch done when every envelope workgroup has counted itself: the last re-zeroes the counters
+    // for the next launch on this plan (stream-ordered after this one)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long prev =
+          __hip_atomic_fetch_add(ho->done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev + 1 == ho->quota_done) {
+        for (int i = 0; i < P->m * ho->rt; ++i)
+          __hip_atomic_store(ho->cnt1 + (size_t)i * HANDOFF_STRIDE, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < ho->nrb; ++i)
+          __hip_atomic_store(ho->cnt2 + (size_t)i * HANDOFF_STRIDE, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ho->done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   if (st) __syncthreads();  // workgroup-uniform: the end stamp covers every wave
   KST_END(st);
+}
+
+template <int MAXL, int M, bool GRAD, bool STREAM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(MAXL, M, GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
+                                                       double* __restrict__ pairs_out, int dst,
+                                                       const double* __restrict__ xnew, double* __restrict__ dkg,
+                                                       const double* __restrict__ mu_all,
+                                                       const double* __restrict__ cov_all,
+                                                       const double* __restrict__ var_all,
+                                                       const double* __restrict__ mux_all,
+                                                       const double* __restrict__ wts, long long cov_stride,
+                                                       int bpad) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
+  envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
+                                       cov_stride, bpad, blockIdx.x, blockIdx.y, gridDim.y, smem, kst_slot(dst, P, 2));
 }
 
 // The lines of every (candidate, scalarisation) pair of the plan's last

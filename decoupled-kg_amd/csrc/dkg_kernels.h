@@ -55,6 +55,10 @@ struct Plan {
   float* root32[DKG_MAX_OUTPUTS];   // F32: quad-packed R^T (fp32 copy of root_frag, plan init)
   float* disc32[DKG_MAX_OUTPUTS];   // F32: quad-packed Q_D (fp32 copy of disc_frag, plan init)
   int* hull_pairs;                  // [max_B x S] upper-envelope lines per pair (written with kg_pairs)
+  int32_t fused;                    // dkg_plan_forward runs the fused one-launch forward (dkg_fused.h)
+  unsigned long long* sync;         // fused hand-off counters: cnt1 [m][rt], cnt2 [nrb], done (zeroed)
+  int* sync_err;                    // fused waits that gave up (bits), after the counters
+  size_t sync_bytes;                // bytes of the counter block (sync .. sync_err), a multiple of 16
 };
 
 // By-value arguments of the state-preparation use of the cross stage.
@@ -90,6 +94,12 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
                         hipStream_t s, int stage);
 hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
                           hipStream_t s, hipEvent_t* ev);
+// The fused one-launch forward (dkg_fused.h) when the plan allows it (Plan::fused, no kg_pairs);
+// otherwise the three stage kernels.  Same bits.
+// Dynamic LDS bytes of the fused forward for a plan (dkg_fused.h fused_lds_bytes).
+size_t fused_lds_bytes_host(const Plan& h);
+hipError_t launch_forward_auto(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg,
+                               double* pairs, hipStream_t s);
 // Envelope stage alone over P sets of L lines: KG, envelope sizes (nullable) and, when idx is given, the
 // reference walk's indices [P][cap] and intersections [P][cap - 1] (lines_kg_kernel / lines_walk_kernel).
 hipError_t launch_lines_kg(const double* a, const double* b, int P, int L, double* kg, int* nhull, long long* idx,

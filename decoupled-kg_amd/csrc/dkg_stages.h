@@ -1,0 +1,492 @@
+// The two contraction stages of the Discrete-KG forward as device functions (gfx950):
+// cross_root_impl (Q_X = K(x, X) R, the means) and posterior_cov_body (the covariance
+// rows), shared by their own kernels (dkg_kernels.hip) and by the fused one-launch
+// forward (dkg_fused.h).
+#pragma once
+
+#include "dkg_device.h"
+
+namespace dkg {
+
+// Element-type plumbing of the two contractions (T = double: the reference's
+// fp64; T = float: DKG_PLAN_F32): accumulator vector, MFMA, fragment words.
+template <class T> struct AccT;
+template <> struct AccT<double> { typedef d4 type; };
+template <> struct AccT<float> { typedef f4 type; };
+__device__ __forceinline__ d4 mfma_t(double a, double b, d4 c) { return mfma_f64(a, b, c); }
+__device__ __forceinline__ f4 mfma_t(float a, float b, f4 c) { return mfma_f32(a, b, c); }
+// k-blocks per 16-byte fragment word
+template <class T> constexpr int kpack() { return sizeof(T) == 8 ? 2 : 4; }
+template <class T>
+__host__ __device__ inline size_t fragT_index(int t, int kb, int l, int KB) {
+  if constexpr (sizeof(T) == 8) return frag_index(t, kb, l, KB);
+  else return frag32_index(t, kb, l, KB);
+}
+// Row of the 16x16 MFMA result held by lane l in accumulator register r.
+template <class T>
+__device__ __forceinline__ int mfma_drow(int l, int r) {
+  if constexpr (sizeof(T) == 8) return (l >> 4) + 4 * r;
+  else return 4 * (l >> 4) + r;
+}
+// lane's operands of the kpack<T>() k-blocks of word j of tile `tile` into out[0 ..)
+template <class T>
+__device__ __forceinline__ void frag_word(const T* __restrict__ base, int tile, int j, int lane, int KB, T* out) {
+  if constexpr (sizeof(T) == 8) {
+    const double2 v = frag_pair(base, tile, j, lane, KB);
+    out[0] = v.x; out[1] = v.y;
+  } else {
+    const float4 v = frag_quad(base, tile, j, lane, KB);
+    out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cross_root_kernel: one workgroup per (16-row tile ti, group c of tile pairs,
+// output).  A pair is (p, T-1-p) of 16-column tiles of Q = K_x R; R upper
+// triangular means tile tj only needs k-blocks kb < 4(tj+1), so pairing the
+// shortest with the longest tile balances the MFMA count.  Group c holds
+// pairs CR_PAIRS c .. CR_PAIRS c + CR_PAIRS - 1: the training inputs are
+// staged in LDS and the K(x, X) tile is evaluated once into LDS in B-operand
+// order for the group's widest pair, then each pair's k range is split over
+// the 8 waves (split-K) with every operand of a wave's chunk loaded before its
+// MFMAs (the next pair's first batch is loaded while this pair's partials are
+// reduced); partials are reduced in LDS in fixed wave order (deterministic).
+// One pair per workgroup evaluates the kernel 6.25x over at n = 256 (the fill
+// is half of a workgroup's lifetime), but four pairs per workgroup made the
+// launch 11 us instead of 6 and lowered the forwards-in-flight throughput
+// (10.46 M against 11.01 M KG-evals/s, profiles/r02/r02za): with a few
+// forwards in flight the stage's latency, not its summed workgroup time,
+// sets the rate.  CR_PAIRS stays a tuning constant.
+#ifndef DKG_CR_WAVES
+#define DKG_CR_WAVES 8
+#endif
+constexpr int CR_WAVES = DKG_CR_WAVES;
+constexpr int CR_U = 8;      // k-blocks per load batch
+constexpr int CR_PAIRS = 1;  // tile pairs per workgroup
+
+// LDS (doubles): the K tile [KB][64], the pair partials (their own region when
+// a workgroup reduces several pairs; else overlaying the K tile), the mean
+// partials, the staged inputs and alpha.  Pairs per workgroup: CR_PAIRS when
+// that fits the CU's 160 KiB, else 1 (large n with large d).
+__host__ __device__ inline size_t cross_lds_doubles(int np, int d, bool sep) {
+  const size_t kb = (size_t)(np / 4) * 64, pt = (size_t)CR_WAVES * 8 * 64;
+  return (sep ? kb + pt : (kb > pt ? kb : pt)) + CR_WAVES * 16 + (size_t)np * d + np;
+}
+__host__ __device__ inline int cross_pairs(int np, int d) {
+  return cross_lds_doubles(np, d, true) * sizeof(double) <= 160 * 1024 ? CR_PAIRS : 1;
+}
+__host__ __device__ inline int cross_groups(int np, int d) {
+  return ((np / 16 + 1) / 2 + cross_pairs(np, d) - 1) / cross_pairs(np, d);
+}
+
+// WT: the forward's Q_X / mean stores write-through (sc1), for the fused forward's hand-off (st_out).
+// GRAD: the same contraction with the kernel replaced by its derivative in
+// the candidate's coordinate `gdim` (J = dK(x, X)/dx_g R, dmean = dK/dx_g alpha).
+// T = float (DKG_PLAN_F32): R^T and Q in fp32 (quad-packed), fp32 MFMA; the
+// kernel evaluations and the mean stay fp64.
+// qx_rm (fp64 forward only): also write Q row-major [rows_pad][n_pad] (the gradient envelope's rows).
+template <int DM, bool GRAD = false, class ET = double, bool WT = false>
+__device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
+                                                ET* __restrict__ qout, double* __restrict__ mout, int ti, int grp,
+                                                double* smem, unsigned long long* st = nullptr, int gdim = 0,
+                                                const double* __restrict__ /*unused*/ = nullptr,
+                                                double* __restrict__ qx_rm = nullptr,
+                                                const ET* __restrict__ root = nullptr) {
+  static_assert(!GRAD || sizeof(ET) == 8, "the gradient stage is fp64");
+  constexpr int QW = kpack<ET>();
+  if constexpr (sizeof(ET) == 8) root = o.root_frag;
+  const int n = o.n;
+  const int np = pad16(n);
+  const int T = np / 16;
+  const int KB = np / 4;
+  const int P = (T + 1) / 2;
+  const int ppg = cross_pairs(np, d);
+  const int pb = grp * ppg, pe = min(P, pb + ppg);
+  if (pb >= pe) return;
+  const int kbW = 4 * (T - pb);           // k-block extent of the group's widest pair (its tile T-1-pb)
+  const int ncol = min(n, 4 * kbW);       // training columns the group needs
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  ET* kb_lds = reinterpret_cast<ET*>(smem);     // [KB][64]
+  const bool sep = ppg > 1;
+  double* part = sep ? smem + KB * 64 : smem;   // [CR_WAVES][8][64] pair partials (cross_lds_doubles)
+  double* mred = smem + (sep ? KB * 64 + CR_WAVES * 8 * 64 : max(KB * 64, CR_WAVES * 8 * 64));  // [CR_WAVES][16]
+  double* xs = mred + CR_WAVES * 16;            // [np][d] staged training inputs
+  double* als = xs + (size_t)np * d;            // [np] alpha
+
+  // a pair's geometry for this wave: tiles, k-block extents, the wave's k chunk
+  // (k-block ranges are even: kbA, kbB are multiples of 4 and chunk is even)
+  struct PairK {
+    int tA, tB, kbA, kbB, k0, k1;
+  };
+  auto pair_k = [&](int p) {
+    PairK q;
+    q.tA = p;
+    q.tB = T - 1 - p;  // tA <= tB
+    q.kbA = 4 * (q.tA + 1);
+    q.kbB = 4 * (q.tB + 1);
+    const int chunk = QW * ((q.kbB / QW + CR_WAVES - 1) / CR_WAVES);
+    q.k0 = wave * chunk;
+    q.k1 = min(q.kbB, q.k0 + chunk);
+    return q;
+  };
+  ET ra[CR_U], rb[CR_U];
+  auto load_batch = [&](const PairK& q, int base) {
+#pragma unroll
+    for (int u = 0; u < CR_U; u += QW) {
+      const int j = min(base + u, q.kbB - QW) / QW;
+      frag_word<ET>(root, q.tB, j, lane, KB, rb + u);
+      frag_word<ET>(root, q.tA, min(j, q.kbA / QW - 1), lane, KB, ra + u);
+    }
+  };
+  // R fragments of this wave's first k-block batch of the first pair: loaded
+  // before anything else so their latency overlaps the staging and the fill.
+  PairK cur = pair_k(pb);
+  load_batch(cur, cur.k0);
+
+  KST(st, 2);
+  const bool want_mean = (mout != nullptr) && (pb == 0);  // pair 0 covers every column
+  // training inputs staged pre-scaled by 1/lengthscale (GPyTorch divides both
+  // inputs by the lengthscale before the distance)
+  for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e] * o.inv_lengthscale[e % d];
+  if (want_mean)
+    for (int e = tid; e < ncol; e += CR_WAVES * WAVE) als[e] = o.alpha[e];
+  const int row = ti * 16 + (lane & 15);
+  const bool rv = row < rows;
+  const int rowc = min(row, rows - 1);
+  double xr[DM];  // the candidate row, pre-scaled (clamped loads, no branches)
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    const int kk = min(k, d - 1);
+    xr[k] = x[(size_t)rowc * d + kk] * o.inv_lengthscale[kk];
+  }
+  __syncthreads();
+
+  KST(st, 3);
+  // ---- fill K(x_row, X_col), col < 4*kbW, in B-operand order (zero outside)
+  double mpart = 0.0;
+  const double os = o.outputscale;
+  const double ilg = GRAD ? o.inv_lengthscale[gdim] : 1.0;
+  double xg = 0.0;  // the candidate's pre-scaled coordinate gdim (GRAD)
+#pragma unroll
+  for (int k = 0; k < DM; ++k) xg = (k == gdim) ? xr[k] : xg;
+  const int fill = kbW * 64;
+  const int iters = (fill + CR_WAVES * WAVE - 1) / (CR_WAVES * WAVE);  // uniform trip count
+  // one straight-line loop per covariance family (the switch stays outside)
+  auto fill_loop = [&](auto kind_c) {
+    constexpr int KIND = decltype(kind_c)::value;
+    const const_dptr tab = psi_tab();
+#pragma unroll 4
+    for (int it = 0; it < iters; ++it) {
+      const int e = tid + it * CR_WAVES * WAVE;
+      const int col = 4 * (e >> 6) + (lane >> 4);
+      const int cc = min(col, n - 1);
+      double r2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < DM; ++k) {
+        const double t = xr[k] - xs[(size_t)cc * d + min(k, d - 1)];
+        r2 = fma(t, (k < d) ? t : 0.0, r2);
+      }
+      double kv;
+      if constexpr (GRAD) {
+        kv = os * kernel_dprofile_t<KIND>(r2) * (xg - xs[(size_t)cc * d + gdim]) * ilg;
+      } else {
+        kv = os * kernel_profile_t<KIND>(r2, tab);
+      }
+      const double v = (rv && col < n) ? kv : 0.0;
+      const double al = als[cc];  // staged only when want_mean; otherwise ignored
+      mpart = fma(v, want_mean ? al : 0.0, mpart);
+      if (e < fill) kb_lds[e] = (ET)v;
+    }
+  };
+  switch (o.kernel) {
+    case DKG_MATERN12: fill_loop(std::integral_constant<int, DKG_MATERN12>{}); break;
+    case DKG_MATERN32: fill_loop(std::integral_constant<int, DKG_MATERN32>{}); break;
+    case DKG_RBF: fill_loop(std::integral_constant<int, DKG_RBF>{}); break;
+    default: fill_loop(std::integral_constant<int, DKG_MATERN52>{}); break;
+  }
+  // mean partials: lanes l, l^16, l^32, l^48 share a row.
+  if (want_mean) {
+    mpart += partner_f64<4>(mpart);
+    mpart += partner_f64<5>(mpart);
+    if (lane < 16) mred[wave * 16 + lane] = mpart;
+  }
+  __syncthreads();
+
+  KST(st, 4);
+  typedef typename AccT<ET>::type acc_t;
+  for (int p = pb; p < pe; ++p) {
+    // ---- split-K MFMA over the pair, loads batched ahead of the MFMAs
+    acc_t accA2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    acc_t accB2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    const bool pairA = cur.tA != cur.tB;
+    for (int base = cur.k0; base < cur.k1; base += CR_U) {
+      ET bo[CR_U];
+      if (base != cur.k0) load_batch(cur, base);
+#pragma unroll
+      for (int u = 0; u < CR_U; ++u) {
+        const int kb = min(base + u, cur.kbB - 1);
+        bo[u] = (base + u < cur.k1) ? kb_lds[kb * 64 + lane] : (ET)0;
+      }
+#pragma unroll
+      for (int u = 0; u < CR_U; ++u) {
+        accB2[u & 1] = mfma_t(rb[u], bo[u], accB2[u & 1]);
+        if (pairA && base + u < cur.kbA) accA2[u & 1] = mfma_t(ra[u], bo[u], accA2[u & 1]);
+      }
+    }
+    const acc_t accA = accA2[0] + accA2[1];
+    const acc_t accB = accB2[0] + accB2[1];
+    const PairK done = cur;
+    if (p + 1 < pe) {  // the next pair's first batch, in flight during this pair's reduction
+      cur = pair_k(p + 1);
+      load_batch(cur, cur.k0);
+    }
+    __syncthreads();  // every wave is done with the previous pair's partials (and, overlaid, with kb_lds)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      part[(wave * 8 + r) * 64 + lane] = (double)accA[r];
+      part[(wave * 8 + 4 + r) * 64 + lane] = (double)accB[r];
+    }
+    __syncthreads();
+
+    // ---- reduce partials in fixed wave order; wave w < 8 finalises (tile, reg) = w.
+    const int tsel = wave >> 2;  // 0 -> tA, 1 -> tB
+    const int r = wave & 3;
+    if (wave < 8 && (tsel == 1 || pairA)) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < CR_WAVES; ++w) s += part[(w * 8 + tsel * 4 + r) * 64 + lane];
+      const int tj = tsel ? done.tB : done.tA;
+      // D = R^T K^T: lane holds Q[16ti + (l&15)][16tj + 4r + (l>>4)] = q_frag[ti][4tj + r][l]
+      if constexpr (GRAD) {
+        // J row-major [bpad][np] for the envelope's per-candidate row loads;
+        // the gdim == 0 workgroups also copy Q_X's matching entries row-major
+        const size_t rm = (size_t)(16 * ti + (lane & 15)) * np + 16 * tj + 4 * r + (lane >> 4);
+        qout[rm] = s;
+      } else {
+        // D row dr = column 16 tj + dr of Q: k-block 4 tj + dr/4, operand lane (l & 15) | (dr % 4) << 4
+        const int dr = mfma_drow<ET>(lane, r);
+        st_out<WT>(&qout[fragT_index<ET>(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)], (ET)s);
+        if constexpr (sizeof(ET) == 8)
+          if (qx_rm) qx_rm[(size_t)(16 * ti + (lane & 15)) * np + 16 * tj + dr] = s;
+      }
+    }
+  }
+  KST(st, 5);
+  if (want_mean && tid < 16) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < CR_WAVES; ++w) s += mred[w * 16 + tid];
+    const int rr = ti * 16 + tid;
+    st_out<WT>(&mout[rr], (rr < rows) ? (GRAD ? s : o.mean_constant + s) : 0.0);
+  }
+  KST_END(st);
+}
+
+// ---------------------------------------------------------------------------
+// posterior_cov_kernel: cov[b][k] = s k(x_b, D_k) - sum_l Q[b][l] Q_D[k][l]
+// One workgroup (8 waves, 2 per SIMD) per 32 x 32 block = 2 x 2 output
+// tiles of one output; wave w computes tile (w % 4) over K part (w / 4) of
+// PC_KS = 2.
+// Waves that share an operand tile and a K-half read it at the same time, so
+// a CU fetches each operand byte about once (L1); every load is a 16-byte
+// pair (two k-blocks).  K parts meet in LDS in fixed order; the part-0
+// wave evaluates the kernel epilogue and stores.  Tiles with tk == 0 also produce the
+// candidates' own variances s - |Q_X[b]|^2.  At <= 128 VGPRs and 8 waves a
+// block shares its CU with another block or an envelope workgroup (also 8
+// waves at <= 128 VGPRs) of another forward in flight: 16 waves (K quarters,
+// 4 per SIMD) kept the block's lifetime and took the CU alone, and lowered
+// the forwards-in-flight throughput from 11.0 M to 9.0 M KG-evals/s
+// (profiles/r02/r02zc); a 64 x 32 block of 16 waves likewise (r02x).
+constexpr int PC_WAVES = 8;
+constexpr int PC_RB = 2;  // 16-row tiles per workgroup (32 candidates); 2 column tiles (32 lines)
+constexpr int PC_KS = PC_WAVES / (2 * PC_RB);  // K splits: the waves of one tile
+constexpr int PC_P = 8;  // 16-byte words per operand per load batch (16 k-blocks)
+
+// T = float (DKG_PLAN_F32): the contraction Q_X . Q_D in fp32 (quad-packed
+// operands, v_mfma_f32_16x16x4_f32); the kernel term, the subtraction and the
+// variance sums (of the fp32 Q_X entries) in fp64.
+template <int DM, class T = double, bool HO = false>
+__device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, const double* __restrict__ xnew, int B,
+                                                   int bx, int by, int oi, double* part, double* qpart,
+                                                   unsigned long long* st, const Handoff* ho = nullptr) {
+  constexpr int QW = kpack<T>();
+  typedef typename AccT<T>::type acc_t;
+  constexpr int NT = 2 * PC_RB;  // output tiles per workgroup
+  KST_BEGIN(st);
+  const dkg_output& o = P->o[oi];
+  const int N = P->N;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tt = wave % NT, ks = wave / NT;
+  const int ti = PC_RB * by + (tt >> 1);
+  const int tk = 2 * bx + (tt & 1);
+  const int KB = pad16(o.n) / 4;
+  const bool have_d = N > 0;
+  // tiles that exist in the workspace / state buffers (wave-uniform)
+  const bool live = ti * 16 < pad16(B) && (tk * 16 < pad16(N) || (tk == 0 && !have_d));
+  const bool want_var = tk == 0;
+  // K part of this wave, in whole 16-byte words (QW k-blocks each)
+  const int KP = KB / QW;
+  const int KPs = (KP + PC_KS - 1) / PC_KS;
+  const int p0 = min(KP, ks * KPs), p1 = min(KP, p0 + KPs);
+  const T* qx;
+  const T* qd;
+  if constexpr (sizeof(T) == 8) {
+    qx = P->q[oi];
+    qd = o.disc_frag;
+  } else {
+    qx = P->q32[oi];
+    qd = P->disc32[oi];
+  }
+
+  // The first batch of contraction operands is loaded first and the epilogue's
+  // inputs after it, so both memory round trips overlap (row b = 16 ti + (l >> 4) + 4 r,
+  // column k = 16 tk + (l & 15)).  HO (fused forward): Q_X is handed off by the cross
+  // workgroups of this launch, so only Q_D's first batch is loaded ahead; Q_X after the wait.
+  const int d = P->d;
+  const int k = tk * 16 + (lane & 15);
+  // disc_frag tile 0 exists only when N == 0: the N == 0 variance-only
+  // wave reads its own Q_X tile as a stand-in (multiplied by 0 below)
+  const T* dsrc = have_d ? qd : qx;
+  const int dt = have_d ? tk : ti;
+  T va[PC_P][QW], vd[PC_P][QW];
+  auto load_x = [&](int pb) {
+#pragma unroll
+    for (int u = 0; u < PC_P; ++u) frag_word<T>(qx, ti, min(pb + u, p1 - 1), lane, KB, va[u]);
+  };
+  auto load_d = [&](int pb) {
+#pragma unroll
+    for (int u = 0; u < PC_P; ++u) frag_word<T>(dsrc, dt, min(pb + u, p1 - 1), lane, KB, vd[u]);
+  };
+  auto load_batch = [&](int pb) {
+#pragma unroll
+    for (int u = 0; u < PC_P; ++u) {
+      const int j = min(pb + u, p1 - 1);
+      frag_word<T>(qx, ti, j, lane, KB, va[u]);
+      frag_word<T>(dsrc, dt, j, lane, KB, vd[u]);
+    }
+  };
+  // The epilogue's kernel terms s k(x_b, D_k), evaluated by the K-part-0 waves before the
+  // contraction: their VALU work overlaps the K-part-1 waves' MFMAs on the same SIMDs (splitting
+  // the terms over both parts overlapped nothing and lengthened the block: profiles/r02/r02zm).
+  // At small d (EPI_FIRST) their inputs are loaded ahead of the first operand batch: loads
+  // complete in order, so the terms' wait does not include the batch and their VALU work overlaps
+  // its round trip.  At larger d the inputs would stay live beside the batch (over 128 VGPRs).
+  constexpr bool EPI_FIRST = DM <= 2;
+  constexpr int RV = 4;
+  const bool epi = ks == 0;  // wave-uniform
+  // line k's coordinates (P->disc is valid even when N == 0: plan init)
+  auto disc_row = [&]() { return P->disc + (size_t)min(k, max(N, 1) - 1) * d; };
+  double ek[EPI_FIRST ? DM : 1], eb[RV][EPI_FIRST ? DM : 1];
+  if (EPI_FIRST && epi) {
+    const double* xk = disc_row();
+#pragma unroll
+    for (int c = 0; c < DM; ++c) {
+      ek[c] = xk[min(c, d - 1)];
+#pragma unroll
+      for (int rr = 0; rr < RV; ++rr)
+        eb[rr][c] = xnew[(size_t)min(ti * 16 + mfma_drow<T>(lane, rr), B - 1) * d + min(c, d - 1)];
+    }
+  }
+  if constexpr (HO) {
+    if (live && p0 < p1) load_d(p0);
+  } else {
+    if (live && p0 < p1) load_batch(p0);
+  }
+  double kv[RV] = {};
+  if (epi) {
+    const double os = o.outputscale;
+    const int kind = o.kernel;
+    const const_dptr tab = psi_tab();
+#pragma unroll
+    for (int rr = 0; rr < RV; ++rr) {
+      double r2;
+      if constexpr (EPI_FIRST) {
+        r2 = 0.0;  // scaled_r2_dm's arithmetic on the preloaded inputs
+#pragma unroll
+        for (int c = 0; c < DM; ++c) {
+          const double t = (eb[rr][c] - ek[c]) * o.inv_lengthscale[min(c, d - 1)];
+          r2 = fma(t, (c < d) ? t : 0.0, r2);
+        }
+      } else {
+        const int b = ti * 16 + mfma_drow<T>(lane, rr);
+        r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, disc_row(), o.inv_lengthscale, d);
+      }
+      kv[rr] = os * kernel_profile(kind, r2, EPI_FIRST ? tab : psi_tab());
+    }
+  }
+  if constexpr (HO) {
+    // Q_X of this block's row tiles (cross workgroups of this launch): both tiles' arrivals, then one acquire
+    const int rt0 = PC_RB * by;
+    const int nrt = min(PC_RB, pad16(B) / 16 - rt0);
+    handoff_wait(ho->cnt1 + ((size_t)oi * ho->rt + rt0) * HANDOFF_STRIDE, nrt, ho->quota1, ho->err, 1);
+    if (live && p0 < p1) load_x(p0);
+  }
+  KST(st, 2);
+  acc_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  double qsq = 0.0;  // lane l: sum over this wave's k of Q_X[16 ti + (l & 15)][k]^2
+  if (live) {
+    for (int pb = p0; pb < p1; pb += PC_P) {
+      if (pb != p0) load_batch(pb);
+#pragma unroll
+      for (int u = 0; u < PC_P; ++u) {
+        const bool in = pb + u < p1 && have_d;
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const T a = va[u][q], dd = in ? vd[u][q] : (T)0;
+          acc[(QW * u + q) & 3] = mfma_t(a, dd, acc[(QW * u + q) & 3]);
+          if (want_var) qsq = (pb + u < p1) ? fma((double)a, (double)a, qsq) : qsq;
+        }
+      }
+    }
+  }
+  const acc_t accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  KST(st, 3);
+  if (want_var) {
+    qsq += __shfl_xor(qsq, 16);
+    qsq += __shfl_xor(qsq, 32);
+  }
+  if (ks > 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[(((ks - 1) * NT + tt) * 4 + r) * 64 + lane] = (double)accs[r];
+    if (want_var && lane < 16) qpart[((ks - 1) * NT + tt) * 16 + lane] = qsq;
+  }
+  __syncthreads();
+  KST(st, 4);
+  if (ks == 0 && live) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double sum = (double)accs[r];
+#pragma unroll
+      for (int q = 0; q < PC_KS - 1; ++q) sum += part[((q * NT + tt) * 4 + r) * 64 + lane];  // fixed order
+      const int b = ti * 16 + mfma_drow<T>(lane, r);
+      if (b < B && k < N)  // line record k of candidate b, component oi (dkg_device.h cov_rec)
+        st_out<HO>(&P->cov_all[(size_t)b * P->cov_stride + (size_t)k * cov_rec(P->m) + oi], kv[r] - sum);
+    }
+    if (want_var && lane < 16) {
+      const int bb = ti * 16 + lane;
+      double qs = qsq;
+#pragma unroll
+      for (int q = 0; q < PC_KS - 1; ++q) qs += qpart[(q * NT + tt) * 16 + lane];
+      if (bb < B) st_out<HO>(&P->var[oi][bb], o.outputscale - qs);
+    }
+  }
+  if constexpr (HO) handoff_publish(ho->cnt2 + (size_t)by * HANDOFF_STRIDE);  // this block's cov_all / var rows are out
+  KST_END(st);
+}
+
+template <int DM, class T = double>
+__global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
+                                                                         const double* __restrict__ xnew, int B,
+                                                                         int dst) {
+  __shared__ __attribute__((aligned(16))) double part[(PC_KS - 1) * 2 * PC_RB * 4 * 64];  // K-split 1.. partial tiles
+  __shared__ double qpart[(PC_KS - 1) * 2 * PC_RB * 16];
+  unsigned long long* st = kst_slot(dst, P, 1);
+  if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1)) return;  // ablation: empty covariance stage
+  posterior_cov_body<DM, T>(P, xnew, B, blockIdx.x, blockIdx.y, blockIdx.z, part, qpart, st);
+}
+
+}  // namespace dkg

@@ -17,10 +17,11 @@ from .errors import BotorchTensorDimensionError, DkgNativeError, NotPSDError, Un
 LIB_PATH = os.environ.get("DKG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native",
                                                      "libdkg.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 DKG_PLAN_GRAD = 1
 DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
 DKG_PLAN_F32 = 4  # fp32 contractions (BASELINE configs[4]); forward only
+DKG_PLAN_FUSED = 8  # the forward as one launch with in-launch hand-offs (dkg_fused.h); not the default
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 
@@ -77,6 +78,8 @@ SIGNATURES = {
     "dkg_plan_time_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                     c_int, POINTER(c_float)]),
     "dkg_plan_hull_sizes": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "dkg_plan_status": (c_int, [c_void_p, POINTER(c_int), c_int, c_void_p]),
+    "dkg_plan_fused": (c_int, [c_void_p]),
     "dkg_lines_kg": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_epigraph": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dkg_pwl_expectation": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

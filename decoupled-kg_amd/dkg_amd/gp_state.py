@@ -127,8 +127,8 @@ class DeviceGPState:
         self._ws_key = None
 
     def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False, force_walk: bool = False,
-             f32: bool = False) -> "ForwardPlan":
-        return ForwardPlan(self, W, target, max_B, grad, force_walk, f32)
+             f32: bool = False, fused: bool = False) -> "ForwardPlan":
+        return ForwardPlan(self, W, target, max_B, grad, force_walk, f32, fused)
 
     def forward(self, X: torch.Tensor, W: torch.Tensor, target, kg_pairs=None, timed: bool = False):
         """One-shot forward (builds a plan on the fly); see ForwardPlan for the fast path."""
@@ -139,12 +139,14 @@ class DeviceGPState:
 class ForwardPlan:
     """A DKG plan (include/dkg.h "Plan API"): weights, target and workspace for
     up to ``max_B`` candidates, device copy written once; ``forward`` is one
-    C call that launches the three kernels on the current stream.  With
-    ``grad=True`` the workspace also holds the gradient buffers and
-    ``forward_grad`` returns dKG/dx alongside KG."""
+    C call that launches the forward on the current stream: the three stage
+    kernels, or with ``fused=True`` one launch whose stages hand off inside it
+    (dkg_fused.h; same bits, not faster on MI355X: DESIGN.md 4.8).  With ``grad=True`` the
+    workspace also holds the gradient buffers and ``forward_grad`` returns
+    dKG/dx alongside KG."""
 
     def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int, grad: bool = False,
-                 force_walk: bool = False, f32: bool = False):
+                 force_walk: bool = False, f32: bool = False, fused: bool = False):
         lib = _lib.load()
         self.state = state
         self.device = state.device
@@ -160,7 +162,7 @@ class ForwardPlan:
         self.grad = bool(grad)
         self.f32 = bool(f32)
         flags = ((_lib.DKG_PLAN_GRAD if self.grad else 0) | (_lib.DKG_PLAN_FORCE_WALK if force_walk else 0)
-                 | (_lib.DKG_PLAN_F32 if self.f32 else 0))
+                 | (_lib.DKG_PLAN_F32 if self.f32 else 0) | (_lib.DKG_PLAN_FUSED if fused else 0))
         need = lib.dkg_plan_workspace(state.structs, state.m, state.d, state.N, self.max_B, self.S, flags)
         self.ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
         nbytes = lib.dkg_plan_bytes()
@@ -170,9 +172,18 @@ class ForwardPlan:
                                      self.S, self.target, self.max_B, flags, _lib.ptr(self.ws), self.ws.numel(),
                                      self.host, _lib.ptr(self.dev), current_stream_ptr(self.device)),
                    "dkg_plan_init")
+        self.fused = bool(lib.dkg_plan_fused(self.host))  # forward_into is one fused launch
         self._fwd = lib.dkg_plan_forward
         self._fwd_timed = lib.dkg_plan_forward_timed
         self._dev_ptr = _lib.ptr(self.dev)
+
+    def status(self, reset: bool = False) -> int:
+        """The bits of the fused launches' in-launch waits that gave up since the last reset (0: every hand-off
+        matched; dkg_plan_status); synchronises the plan's stream."""
+        err = ctypes.c_int(0)
+        _lib.check(_lib.load().dkg_plan_status(self.host, ctypes.byref(err), int(reset),
+                                               current_stream_ptr(self.device)), "dkg_plan_status")
+        return err.value
 
     def forward_into(self, X: torch.Tensor, kg: torch.Tensor, kg_pairs=None) -> None:
         """Hot path: X (device, B x d, contiguous fp64) -> kg (device, B)."""
@@ -289,7 +300,8 @@ class ForwardPlan:
 
     def time_stage(self, X: torch.Tensor, stage: int, reps: int) -> float:
         """Average duration (ms) of ``reps`` back-to-back launches of one kernel
-        (0 cross_root, 1 posterior_cov, 2 envelope), HIP events on the launch stream."""
+        (0 cross_root, 1 posterior_cov, 2 envelope; 3 the whole forward as ``forward_into`` launches it),
+        HIP events on the launch stream."""
         X = X.detach().to(self.device, torch.double).contiguous()
         kg = torch.empty(X.shape[0], dtype=torch.double, device=self.device)
         ms = _lib.c_float()

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 3
+#define DKG_ABI_VERSION 4
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -170,13 +170,21 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
  * fp64 plan to ~1e-3 relative when the noise is >= 1e-3 of the outputscale.
  * Forward only (not combinable with DKG_PLAN_GRAD). */
 #define DKG_PLAN_F32 4
+/* DKG_PLAN_FUSED: dkg_plan_forward launches the forward as ONE kernel whose cross,
+ * covariance and envelope workgroups hand the stages on through arrival counters
+ * (dkg_fused.h), instead of the three stage kernels; fp64 plans whose lines fit the
+ * staged envelope (N + 1 <= 1088).  Same bits either way.  Not the default: on
+ * MI355X an in-launch hand-off costs about what the kernel boundary it replaces
+ * does, and the early-dispatched consumers slow the producers. */
+#define DKG_PLAN_FUSED 8
 size_t dkg_plan_bytes(void);
 size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags);
 int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,
                   int target, int max_B, int flags, void* workspace, size_t workspace_bytes, void* host_plan,
                   void* dev_plan, void* stream);
 /* kg[b] (and kg_pairs[b x S], nullable) for B <= max_B candidates xnew (device, B x d);
- * same result as dkg_forward with the plan's arguments. */
+ * same result as dkg_forward with the plan's arguments.  One fused launch for a plan built
+ * with DKG_PLAN_FUSED (a call given kg_pairs runs the three stages). */
 int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                      double* kg_pairs, void* stream);
 /* As dkg_plan_forward with per-kernel HIP-event timings (synchronises): stage_ms[3]. */
@@ -200,8 +208,18 @@ int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const dou
  * pair short-circuits (all |b| < 1e-9, :363-367).  Device int[B x S]; stream
  * ordered.  Diagnostics (log the envelope-size histogram). */
 int dkg_plan_hull_sizes(const void* host_plan, int* out, int B, void* stream);
+/* Hand-off status of the plan's fused launches (DKG_PLAN_FUSED) (stream ordered, synchronises):
+ * *err = the OR of the bits of every in-launch wait that gave up since the last
+ * reset (1 covariance on cross, 2 envelope on covariance; 0 = every wait matched;
+ * a wait that gives up lets its workgroup go on, so the launch ends and its
+ * results are not to be used).  reset != 0: clear the bits and re-zero the arrival
+ * counters.  Returns DKG_OK (or a HIP error). */
+int dkg_plan_status(const void* host_plan, int* err, int reset, void* stream);
+/* 1 if dkg_plan_forward runs the plan's forward as the fused single launch, 0 if as the three stage kernels. */
+int dkg_plan_fused(const void* host_plan);
 /* Benchmark helper: average HIP-event duration (ms) of `reps` back-to-back
- * launches of one stage (0 cross_root, 1 posterior_cov, 2 envelope) on
+ * launches of one stage (0 cross_root, 1 posterior_cov, 2 envelope, 3 the
+ * whole forward as dkg_plan_forward launches it) on
  * `stream`, after one full forward that primes its inputs; a final full
  * forward leaves kg / kg_pairs valid.  Synchronises. */
 int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
