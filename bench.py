@@ -19,15 +19,18 @@ all-gathers the per-candidate values instead.
 
 Prints one JSON line (rank 0): value = KG-evals/s over all ranks, plus
   * ``roofline``: the dominant kernel's duration (HIP events on its launch
-    stream) against the ceiling that binds it: the envelope is
-    VALU-issue bound (it does comparisons and selects, not counted flops), so its
-    fraction is VALU-busy SIMD cycles (PMC count per launch, profiles/) over the
-    SIMD cycles of the live launch; every stage is listed in ``stages``;
+    stream) against the fp64 roof (78.6 TF/s, vector = matrix on MI355X): ``achieved``
+    = SURVEY 8(d)'s counted flops per launch / duration, ``frac`` = achieved / peak;
+    ``valu_busy_frac`` (VALU-busy SIMD cycles per launch from the workload's own PMC
+    file under profiles/, null when there is none) beside it; every stage in ``stages``;
   * ``cpu_baseline``: a bounded sample of the oracle restatement on the host cores;
   * ``nondegenerate``: the same throughput path on headline sizes with KG > 0 for
     every pair (d = 6; the envelope does real work);
+  * ``stress``: the BASELINE configs[4] shape (m 3, n 1024, N 4096, S 32, B 256) in fp64;
   * ``latency_b1``: value+gradient at B = 1, the ``optimize_acqf`` call shape of the
-    reference's production loop (bo_loop.py:127-129, batch_limit=1).
+    reference's production loop (bo_loop.py:127-129, batch_limit=1), through
+    ``value_and_grad_host`` and through ``forward()`` + autograd on a host X;
+  * ``per_rank``: every rank's forward time and its exposed final-collective time.
 """
 
 import argparse
@@ -55,7 +58,7 @@ FP64_VALU_MEASURED_TFLOPS = 61.4
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 SIMDS, CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMDs
-PMC_REPORT = os.path.join(REPO, "profiles", "r02", "pmc_headline.json")
+PMC_DIR = os.path.join(REPO, "profiles", "r03")
 
 
 def parse():
@@ -84,8 +87,11 @@ def parse():
     ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
     ap.add_argument("--nd-steps", type=int, default=256,
                     help="timed steps of the non-degenerate headline-size leg (workload headline_nd; 0 = skip)")
-    ap.add_argument("--pmc", default=PMC_REPORT,
-                    help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py)")
+    ap.add_argument("--pmc", default="auto",
+                    help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py); auto: "
+                         "profiles/r03/pmc_<workload>[_fp32].json, none if that file does not exist")
+    ap.add_argument("--stress-steps", type=int, default=8,
+                    help="timed forwards of the stress leg (BASELINE configs[4] shape, fp64; 0 = skip)")
     return ap.parse_args()
 
 
@@ -153,6 +159,10 @@ def cpu_baseline(model, D, W, X, target, seconds, threads_req):
     dt = time.perf_counter() - t0
     return {"value": cnt / dt, "unit": "KG-evals/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model, "affinity_cpus": aff,
+            # BASELINE.md's plan names len(sched_getaffinity) threads; on the GPU box that is the whole host, of
+            # which one GPU's share is OMP_NUM_THREADS (16), so the sample runs there and this is the linear
+            # upper bound of the same restatement on every CPU of the affinity set (it scales sublinearly)
+            "value_at_affinity_linear_upper_bound": cnt / dt * aff / max(1, threads),
             "sample": f"{cnt} forwards cycling over the {Xc.shape[0]} headline candidates (per-candidate loop, "
                       f"dense (N+1)^2 posterior covariance, reference epigraph walk; torch fp64 CPU, "
                       f"{threads} threads), {dt:.1f} s"}
@@ -309,11 +319,16 @@ class Throughput:
             step(k)
             host += time.perf_counter() - th
         join()
+        evc = torch.cuda.Event(enable_timing=True)
+        evc.record()  # every forward of the timed region enqueued before this point on the main stream
         xchg.flush(steps)
         ev1.record()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         self.host_us_per_step = host / max(1, steps) * 1e6
+        # this rank's device time of the forwards, and what the last exchange adds after them (exposed)
+        self.compute_ms = ev0.elapsed_time(evc)
+        self.exposed_ms = evc.elapsed_time(ev1)
         if world > 1:
             dist.barrier()
         gpu_s = ev0.elapsed_time(ev1) / 1e3
@@ -337,39 +352,35 @@ def batch_stats(plan, Xd):
 
 
 def stage_rooflines(plan, Xd, model_fb, reps, precision, pmc):
-    """Every forward kernel against the ceiling that binds it.  Durations: HIP events around `reps`
-    back-to-back launches of the kernel alone on its own stream (dkg_plan_time_stage)."""
+    """Every forward kernel against the compute roof (fp64 78.6 TF/s; the fp32 MFMA peak for fp32
+    contractions) with its counted flops, and against HBM with its algorithmic bytes.  Durations: HIP
+    events around `reps` back-to-back launches of the kernel alone on its own stream (dkg_plan_time_stage).
+    VALU-busy and traffic come from the workload's PMC file when there is one (else null)."""
     names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
     avg_ms = [plan.time_stage(Xd, k, reps) for k in range(3)]
     out = {}
     for i, name in enumerate(names):
         fl, by = model_fb[name]
         t = avg_ms[i] * 1e-3
-        r = {"avg_launch_us": t * 1e6, "algorithmic_flops": fl, "algorithmic_bytes": by,
-             "hbm_gbs_algorithmic": by / t / 1e9}
         p = pmc.get(name, {})
-        traffic = p.get("hbm_bytes_per_launch")
-        if name == "posterior_cov_kernel":
-            peak = FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else FP64_PEAK_TFLOPS
-            ach = fl / t / 1e12
-            r.update({"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
-                      "frac_of_measured_peak": ach / FP64_MFMA_MEASURED_TFLOPS,
-                      "mfma_busy_frac_pmc": p.get("mfma_busy_frac")})
-        else:
-            # VALU-issue bound: the envelope's comparisons / selects and cross_root's exp / sqrt fill
-            # are not flops; the fraction is VALU-busy SIMD cycles (PMC SQ_ACTIVE_INST_VALU x 4 quad-cycles,
-            # per launch) over the SIMD cycles of this launch
-            busy = p.get("valu_busy_simd_cycles")
-            ach = busy / t if busy else None
-            peak = SIMDS * CLOCK_GHZ * 1e9
-            r.update({"bound": "valu", "achieved": ach, "peak": peak, "unit": "VALU-busy SIMD-cycles/s",
-                      "frac": (ach / peak) if ach else None,
-                      "counted_fp64_tflops": fl / t / 1e12,
-                      "counted_flop_frac_of_valu_peak": fl / t / 1e12 / FP64_VALU_MEASURED_TFLOPS,
-                      "valu_insts_per_wave": p.get("valu_insts_per_wave")})
-        r["traffic"] = traffic
+        peak = FP32_MFMA_PEAK_TFLOPS if (precision == "fp32" and name != "envelope_kernel") else FP64_PEAK_TFLOPS
+        ach = fl / t / 1e12
+        busy = p.get("valu_busy_simd_cycles")
+        r = {"avg_launch_us": t * 1e6, "algorithmic_flops": fl, "algorithmic_bytes": by,
+             "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+             "hbm_gbs_algorithmic": by / t / 1e9, "hbm_frac": by / t / 1e9 / HBM_PEAK_GBS,
+             "traffic": p.get("hbm_bytes_per_launch"),
+             "valu_busy_frac": (busy / t / (SIMDS * CLOCK_GHZ * 1e9)) if busy else None,
+             "mfma_busy_frac_pmc": p.get("mfma_busy_frac"),
+             "valu_insts_per_wave": p.get("valu_insts_per_wave")}
         out[name] = r
     return out
+
+
+def pmc_file(args) -> str:
+    if args.pmc != "auto":
+        return args.pmc
+    return os.path.join(PMC_DIR, f"pmc_{args.workload}{'_fp32' if args.precision == 'fp32' else ''}.json")
 
 
 def main():
@@ -422,21 +433,34 @@ def main():
         single = {"value": world * w.B * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
     elapsed = tp.run(max(1, args.streams), args.steps, args.warmup, args.graph, world)
     value = world * w.B * args.steps / elapsed
+    mine = torch.tensor([tp.compute_ms, tp.exposed_ms, elapsed * 1e3], dtype=torch.double, device=dev)
+    if world > 1:
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+    else:
+        allr = [mine]
+    per_rank = {"compute_ms": [float(r[0]) for r in allr], "exposed_collective_ms": [float(r[1]) for r in allr],
+                "elapsed_ms": [float(r[2]) for r in allr],
+                "what": "compute: HIP events from the start of the timed region to the last forward enqueued; "
+                        "exposed: from there to the end of the final exchange (the collective nothing overlaps)"}
 
     # ---- per-kernel rooflines; the dominant kernel's is the line's `roofline`
     pmc = {}
-    if os.path.exists(args.pmc):
+    pmc_path = pmc_file(args)
+    if os.path.exists(pmc_path):
         try:
-            pmc = json.load(open(args.pmc))
+            pmc = json.load(open(pmc_path))
         except (OSError, ValueError):
             pmc = {}
     model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)
     stages = stage_rooflines(tp.plan, tp.Xd, model_fb, args.profile_reps, args.precision, pmc)
     dom = max(stages, key=lambda k: stages[k]["avg_launch_us"])
     roof = dict(stages[dom], kernel=dom,
-                stages={k: {kk: v[kk] for kk in ("avg_launch_us", "bound", "frac", "traffic")}
+                bound_note="fp64 compute roof: 78.6 TF/s is both the vector and the matrix fp64 peak of MI355X; "
+                           "achieved = SURVEY 8(d) counted flops per launch / launch duration",
+                stages={k: {kk: v[kk] for kk in ("avg_launch_us", "bound", "frac", "valu_busy_frac", "traffic")}
                         for k, v in stages.items()},
-                pmc_source=os.path.relpath(args.pmc, REPO) if pmc else None)
+                pmc_source=os.path.relpath(pmc_path, REPO) if pmc else None)
 
     # ---- whole-forward roofline as BASELINE.md defines it: max(F/P, Bytes/BW) / T_measured
     f_fwd, b_fwd = survey_model(w.m, [mm.num_train for mm in model.models], D.shape[0], w.S, w.B, w.d)
@@ -471,7 +495,10 @@ def main():
                 p1.forward_grad(tp.Xd[:1].contiguous())
                 acq.value_and_grad_host(xh[i:i + 1])
             torch.cuda.synchronize()
-            ts, te = [], []
+            ts, te, ta = [], [], []
+            for i in range(5):  # the autograd route's plans and pinned buffers
+                xa = xh[i:i + 1].unsqueeze(-2).requires_grad_(True)
+                torch.autograd.grad(-acq(xa).sum(), xa)
             for i in range(args.b1_calls):
                 x1 = xh[i % w.B:i % w.B + 1]
                 t0 = time.perf_counter()
@@ -482,10 +509,23 @@ def main():
                 kg1, g1 = p1.forward_grad(xd)
                 kg1.cpu(), g1.cpu()
                 te.append(time.perf_counter() - t0)
+                # what gen_candidates_scipy does per L-BFGS-B evaluation: a host X[1, 1, d] with requires_grad,
+                # the acquisition's forward, autograd back to X (bo_loop.py:127-129 -> optimize_acqf)
+                t0 = time.perf_counter()
+                xa = x1.unsqueeze(-2).requires_grad_(True)
+                loss = -acq(xa).sum()
+                (ga,) = torch.autograd.grad(loss, xa)
+                float(loss), ga.numpy()
+                ta.append(time.perf_counter() - t0)
             ts.sort()
             te.sort()
+            ta.sort()
             lat_b1 = {"median_us": ts[len(ts) // 2] * 1e6, "p90_us": ts[int(len(ts) * 0.9)] * 1e6,
                       "calls": len(ts), "eager_two_copies_median_us": te[len(te) // 2] * 1e6,
+                      "autograd_route": {"median_us": ta[len(ta) // 2] * 1e6, "p90_us": ta[int(len(ta) * 0.9)] * 1e6,
+                                         "what": "host X[1, 1, d].requires_grad_() -> acq(X) -> autograd.grad "
+                                                 "(the unchanged optimize_acqf call; _HostForwardFn: one round "
+                                                 "trip, host backward)"},
                       "what": "value + dKG/dx at one host candidate through the public entry the L-BFGS-B "
                               "objective calls (value_and_grad_host: model check, pinned H2D, 3 launches, one "
                               "pinned D2H), device round trip included; eager_two_copies: the plan's C call on a "
@@ -502,6 +542,20 @@ def main():
               "config": {"m": wn.m, "n_train": wn.n_train, "n_disc": Dn.shape[0], "S": wn.S, "B": wn.B, "d": wn.d,
                          "lengthscales": wn.lengthscales, "outputscales": wn.outputscales, "noise": wn.noise},
               "batch_stats": batch_stats(tpn.plan, tpn.Xd)}
+
+    # ---- stress leg: BASELINE configs[4]'s shape (m 3, n 1024, N 4096, S 32, B 256), fp64
+    stress = None
+    if args.stress_steps > 0 and args.workload == "headline" and args.precision == "fp64":
+        ws, ms, Ds, _, _, _, tps = setup("stress")
+        es = tps.run(1, args.stress_steps, 2, False, world)
+        fb = stage_model(ws, ws.m, [mm.num_train for mm in ms.models], Ds.shape[0], ws.B, ws.S, ws.d)
+        st_s = stage_rooflines(tps.plan, tps.Xd, fb, 3, "fp64", {})
+        stress = {"workload": "stress", "value": world * ws.B * args.stress_steps / es, "unit": "KG-evals/s",
+                  "steps": args.stress_steps, "ms_per_step": es / args.stress_steps * 1e3, "dtype": "f64",
+                  "config": {"m": ws.m, "n_train": ws.n_train, "n_disc": Ds.shape[0], "S": ws.S, "B": ws.B,
+                             "d": ws.d},
+                  "stages": {k: {kk: v[kk] for kk in ("avg_launch_us", "achieved", "frac")} for k, v in st_s.items()}}
+        del tps
 
     out = None
     if rank == 0:
@@ -542,6 +596,8 @@ def main():
             "forward_roofline": fwd_roof,
             "batch_stats": stats,
             "nondegenerate": nd,
+            "stress": stress,
+            "per_rank": per_rank,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

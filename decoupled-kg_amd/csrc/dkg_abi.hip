@@ -492,6 +492,24 @@ int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const dou
                                        (hipStream_t)stream), "forward_grad");
 }
 
+int dkg_plan_forward_grad_hostx(const void* host_plan, const void* dev_plan, const double* x_host, double* x_dev,
+                                int B, double* kg, double* dkg_dx, void* stream) {
+  if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  if (!h.grad) return fail(DKG_ERR_ARG, "plan was not initialised with DKG_PLAN_GRAD");
+  if (B < 0) return fail(DKG_ERR_ARG, "negative B=%d", B);
+  if (B == 0) return DKG_OK;
+  if (B > h.max_B) return fail(DKG_ERR_ARG, "B=%d candidates > plan capacity %d", B, h.max_B);
+  if ((long long)B * h.d > DKG_XARG_MAX)
+    return fail(DKG_ERR_ARG, "B*d=%lld > DKG_XARG_MAX=%d (use dkg_plan_forward_grad)", (long long)B * h.d, DKG_XARG_MAX);
+  if (!x_host || !x_dev || !kg || !dkg_dx) return fail(DKG_ERR_ARG, "NULL data pointer");
+  XArg xa;
+  xa.n = B * h.d;
+  for (int i = 0; i < xa.n; ++i) xa.v[i] = x_host[i];
+  return hip_check(launch_forward_grad(h, static_cast<const Plan*>(dev_plan), x_dev, B, kg, dkg_dx,
+                                       (hipStream_t)stream, &xa), "forward_grad_hostx");
+}
+
 int dkg_plan_status(const void* host_plan, int* err, int reset, void* stream) {
   if (!host_plan || !err) return fail(DKG_ERR_ARG, "NULL pointer");
   const Plan& h = *static_cast<const Plan*>(host_plan);

@@ -4,9 +4,27 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "dkg.h"
 
 namespace dkg {
+
+// Dynamic LDS above the 64 KiB default needs the kernel's limit raised once per (kernel, device):
+// remembered here, so a launch pays a map lookup, not a runtime call (B = 1 latency).
+inline void raise_lds_limit(const void* kernel, size_t lds) {
+  if (lds <= 65536) return;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& cur = done[{kernel, dev}];
+  if (cur >= lds) return;
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess) cur = lds;
+}
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 

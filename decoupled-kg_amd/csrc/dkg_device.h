@@ -1899,9 +1899,7 @@ struct EnvLaunch {
 
 template <int MAXL, int M, bool GRAD, bool STREAM>
 hipError_t launch_env_t(const EnvLaunch& a) {
-  if (a.lds > 65536)
-    (void)hipFuncSetAttribute((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);
+  raise_lds_limit((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>, a.lds);
   const Plan& h = *a.host;
   hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights,

@@ -97,9 +97,7 @@ inline size_t fused_lds_bytes(const Plan& h) {
 
 template <int DM, int MAXL, int M>
 hipError_t launch_fused_t(const FusedArgs& a, size_t lds, hipStream_t s) {
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)forward_fused_kernel<DM, MAXL, M>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  raise_lds_limit((const void*)forward_fused_kernel<DM, MAXL, M>, lds);
   hipLaunchKernelGGL((forward_fused_kernel<DM, MAXL, M>), dim3(a.nC + a.nV + a.B * a.split), dim3(512), lds, s, a);
   return hipGetLastError();
 }

@@ -86,8 +86,13 @@ hipError_t launch_frag_to_f32(const double* frag, int rows, int n, float* out, h
 hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
 // Value and gradient: kg[B] and dkg[B x d] (d KG(x_b) / d x_b), plan built with DKG_PLAN_GRAD.
+// Candidates by value in the first kernel's arguments (dkg_plan_forward_grad_hostx); n = 0: unused.
+struct XArg {
+  double v[DKG_XARG_MAX];
+  int n;
+};
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
-                               hipStream_t s);
+                               hipStream_t s, const XArg* xa = nullptr);
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream);
 // One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,

@@ -106,15 +106,24 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
 // output oi; the first of these workgroups clears the gradient accumulator dkg[B x d].  The two halves
 // read only x and the state, so they run side by side in one launch (at B = 1 the value+gradient chain
 // is latency-bound: one launch and one dependency gap fewer than two cross launches).
+// xa.n > 0 (dkg_plan_forward_grad_hostx): the candidates come in the kernel arguments; every workgroup
+// reads them there, and the first leaves them in xnew for the later kernels of the chain.
 template <int DM>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_fwd_grad_kernel(const Plan* __restrict__ P,
-                                                                         const double* __restrict__ xnew, int B,
+                                                                         double* __restrict__ xstage, int B,
                                                                          double* __restrict__ kg,
-                                                                         double* __restrict__ dkg, int dst) {
+                                                                         double* __restrict__ dkg, int dst,
+                                                                         const XArg xa) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   unsigned long long* st = kst_slot(dst, P, 0);
   const int m = P->m, d = P->d;
   const int z = blockIdx.z;
+  const double* xnew = xstage;
+  if (xa.n > 0) {
+    xnew = xa.v;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && z == 0)
+      for (int i = threadIdx.x; i < xa.n; i += blockDim.x) xstage[i] = xa.v[i];
+  }
   if (z < m) {
     if (blockIdx.x == 0 && blockIdx.y == 0 && z == 0)
       for (int i = threadIdx.x; i < B; i += blockDim.x) {
@@ -312,8 +321,7 @@ static hipError_t launch_cross_root_t(const CrossArgs& a, hipStream_t s) {
   const int np = pad16(a.o.n);
   dim3 grid(pad16(a.rows) / 16, cross_groups(np, a.d), 1);
   const size_t lds = cross_root_lds_bytes(np, a.d);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)cross_root_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  raise_lds_limit((const void*)cross_root_kernel<DM>, lds);
   hipLaunchKernelGGL(cross_root_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, a);
   return hipGetLastError();
 }
@@ -333,9 +341,7 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
   if (stage == 0) {
     dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
-    if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)cross_root_plan_kernel<DM, T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    raise_lds_limit((const void*)cross_root_plan_kernel<DM, T>, lds);
     hipLaunchKernelGGL((cross_root_plan_kernel<DM, T>), grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
                        h.debug_stamp);
     return hipGetLastError();
@@ -392,25 +398,26 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
 
 template <int DM>
 static hipError_t launch_cross_fwd_grad_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
-                                          double* dkg, hipStream_t s) {
+                                          double* dkg, hipStream_t s, const XArg& xa) {
   dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m * (1 + h.d));
   const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)cross_fwd_grad_kernel<DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL(cross_fwd_grad_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg, dkg,
-                     h.debug_stamp);
+  raise_lds_limit((const void*)cross_fwd_grad_kernel<DM>, lds);
+  hipLaunchKernelGGL(cross_fwd_grad_kernel<DM>, grid, dim3(CR_WAVES * WAVE), lds, s, dev,
+                     const_cast<double*>(xnew), B, kg, dkg, h.debug_stamp, xa);
   return hipGetLastError();
 }
 
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
-                               hipStream_t s) {
+                               hipStream_t s, const XArg* xa) {
   hipError_t e;
+  XArg none;
+  none.n = 0;
+  const XArg& x = xa ? *xa : none;
   switch (dim_bucket(h.d)) {  // Q_X (fragment + row-major), means, J_g, dmean; kg = dkg = 0
-    case 2: e = launch_cross_fwd_grad_t<2>(h, dev, xnew, B, kg, dkg, s); break;
-    case 4: e = launch_cross_fwd_grad_t<4>(h, dev, xnew, B, kg, dkg, s); break;
-    case 8: e = launch_cross_fwd_grad_t<8>(h, dev, xnew, B, kg, dkg, s); break;
-    default: e = launch_cross_fwd_grad_t<16>(h, dev, xnew, B, kg, dkg, s); break;
+    case 2: e = launch_cross_fwd_grad_t<2>(h, dev, xnew, B, kg, dkg, s, x); break;
+    case 4: e = launch_cross_fwd_grad_t<4>(h, dev, xnew, B, kg, dkg, s, x); break;
+    case 8: e = launch_cross_fwd_grad_t<8>(h, dev, xnew, B, kg, dkg, s, x); break;
+    default: e = launch_cross_fwd_grad_t<16>(h, dev, xnew, B, kg, dkg, s, x); break;
   }
   if (e != hipSuccess) return e;
   if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 1)) != hipSuccess) return e;  // cov rows, variances

@@ -117,6 +117,26 @@ class _ForwardFn(torch.autograd.Function):
         return grad.to(dkg)[:, None] * dkg, None
 
 
+class _HostForwardFn(torch.autograd.Function):
+    """``forward`` of host candidates (what ``optimize_acqf`` passes: a host X with ``requires_grad``):
+    one device round trip per call -- a pinned H2D copy of X, the forward's launches (with dKG/dx when
+    X requires grad) and one pinned D2H copy of the results -- and a host-side backward.  The same
+    kernels as ``_ForwardFn``, so the same bits."""
+
+    @staticmethod
+    def forward(ctx, X, acq):
+        if ctx.needs_input_grad[0]:
+            kg, dkg = acq._plan_for(X.shape[0], grad=True).forward_grad_host(X)
+            ctx.save_for_backward(dkg)
+            return kg
+        return acq._plan_for(X.shape[0]).forward_host(X)
+
+    @staticmethod
+    def backward(ctx, grad):
+        (dkg,) = ctx.saved_tensors
+        return grad.to(dkg)[:, None] * dkg, None
+
+
 class DiscreteKnowledgeGradient(_Base):
     """Discrete knowledge gradient (C-MOKG), linear scalarisations only."""
 
@@ -223,6 +243,9 @@ class DiscreteKnowledgeGradient(_Base):
                 f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
         self._refresh()
         flat = X.reshape(-1, d)
+        if X.device.type == "cpu":  # the host route: one round trip (and a host backward)
+            kg = _HostForwardFn.apply(flat.to(torch.double).contiguous(), self)
+            return kg.to(dtype=X.dtype).reshape(batch_shape)
         Xd = flat.to(self._state.device, torch.double)
         kg = _ForwardFn.apply(Xd, self)
         return kg.to(device=X.device, dtype=X.dtype).reshape(batch_shape)

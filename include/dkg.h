@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 4
+#define DKG_ABI_VERSION 5
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -202,6 +202,15 @@ int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const do
  * where only the candidate's own line 0 intercept and the slopes depend on x. */
 int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                           double* dkg_dx, void* stream);
+/* Largest B * d of dkg_plan_forward_grad_hostx. */
+#define DKG_XARG_MAX 64
+/* dkg_plan_forward_grad for candidates given in HOST memory (x_host[b*d + j], B * d <= DKG_XARG_MAX):
+ * the candidates travel inside the first kernel's arguments instead of a host-to-device copy
+ * (one copy fewer on the optimize_acqf L-BFGS-B path, batch_limit = 1: bo_loop.py:127-129), and
+ * that kernel leaves them in x_dev (device, B x d) for the later kernels.  x_host may be reused as
+ * soon as this returns.  Same results, bit for bit, as dkg_plan_forward_grad on x_dev. */
+int dkg_plan_forward_grad_hostx(const void* host_plan, const void* dev_plan, const double* x_host, double* x_dev,
+                                int B, double* kg, double* dkg_dx, void* stream);
 /* Envelope sizes of the plan's last forward that was given kg_pairs (same B):
  * out[b*S + j] = the number of upper-envelope lines of pair (b, j), i.e. the
  * len(indices) of calculate_epigraph_indices (discretekg.py:341-412); 1 when the

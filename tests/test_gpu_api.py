@@ -149,3 +149,51 @@ def test_value_and_grad_host_follows_a_refit_model():
     (g_ref,) = torch.autograd.grad(kg_ref.sum(), Xg)
     assert torch.equal(kg1, kg_ref.detach().cpu()) and torch.equal(g1, g_ref.squeeze(-2).cpu())
     assert not torch.equal(kg0, kg1)
+
+
+@pytest.mark.parametrize("B", [1, 3, 16])
+def test_host_route_matches_device_route(B):
+    """forward of a host X (the call optimize_acqf makes: host candidates with requires_grad, then backward)
+    runs _HostForwardFn -- one round trip, host backward -- and gives the device route's bits."""
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=0 if B == 3 else None)
+    for rep in range(2):
+        Xb = X.roll(5 * rep, 0)[:B].clone().reshape(B, 1, 1, 2)  # batch shape (B, 1)
+        Xh = Xb.clone().requires_grad_(True)
+        kg_h = acq(Xh)
+        assert kg_h.device.type == "cpu" and kg_h.shape == (B, 1) and kg_h.requires_grad
+        (g_h,) = torch.autograd.grad((kg_h * 2.0).sum(), Xh)
+        Xd = Xb.to(DEV).requires_grad_(True)
+        kg_d = acq(Xd)
+        (g_d,) = torch.autograd.grad((kg_d * 2.0).sum(), Xd)
+        assert torch.equal(kg_h.detach(), kg_d.detach().cpu())
+        assert torch.equal(g_h, g_d.cpu())
+        # without grad: the forward-only plan, same values as the device route's forward-only plan
+        with torch.no_grad():
+            assert torch.equal(acq(Xb), acq(Xb.to(DEV)).cpu())
+    # float32 host candidates: computed in fp64, returned in the input's dtype (as the device route)
+    X32 = X[:B].float().unsqueeze(-2)
+    assert torch.equal(acq(X32), acq(X32.to(DEV)).cpu())
+    assert acq(X[:0].unsqueeze(-2)).shape == (0,)
+
+
+@pytest.mark.parametrize("B", [1, 10, 11])
+def test_candidates_in_kernel_arguments_match_the_copy_path(B):
+    """forward_grad_host with B * d <= DKG_XARG_MAX passes the candidates in the first kernel's arguments
+    (dkg_plan_forward_grad_hostx); past it, a pinned copy: both give dkg_plan_forward_grad's bits (d = 6:
+    B = 10 is inside, B = 11 past the bound)."""
+    from dkg_amd import _lib
+
+    model, D, X, W = make_problem(WORKLOADS["parity6d"])
+    acq = DiscreteKnowledgeGradient(model, D, W)
+    plan = acq._plan_for(B, grad=True)
+    assert (B * 6 <= _lib.DKG_XARG_MAX) == (B <= 10)
+    for rep in range(3):
+        Xb = X.roll(3 * rep, 0)[:B].clone()
+        kg_ref, g_ref = plan.forward_grad(Xb.to(DEV))
+        kg, g = plan.forward_grad_host(Xb)
+        assert torch.equal(kg, kg_ref.cpu()) and torch.equal(g, g_ref.cpu())
+        # a strided host view of the same candidates
+        Xs = torch.stack([Xb, Xb], -1)[..., 0]
+        kg2, g2 = plan.forward_grad_host(Xs)
+        assert torch.equal(kg2, kg) and torch.equal(g2, g)

@@ -1,0 +1,18 @@
+"""B = 1 value+gradient calls for a kernel trace:  rocprofv3 --kernel-trace --stats -- python3 tools/b1_kernels.py"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "decoupled-kg_amd")]
+import torch  # noqa: E402
+
+from dkg_amd import DiscreteKnowledgeGradient  # noqa: E402
+from dkg_amd.synthetic import WORKLOADS, make_problem  # noqa: E402
+
+w = WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "headline"]
+model, D, X, W = make_problem(w)
+acq = DiscreteKnowledgeGradient(model, D, W)
+for i in range(200):
+    acq.value_and_grad_host(X[i % w.B:i % w.B + 1])
+torch.cuda.synchronize()
+print("done")

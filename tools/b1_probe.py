@@ -62,6 +62,56 @@ for i in range(calls):
     ts.append(time.perf_counter() - t0)
 res["bench"] = med(ts)
 
+# the round trip's parts: the C call + stream sync; + a pinned H2D copy of x first; + a pinned D2H copy after
+stream = torch.cuda.current_stream()
+hx = torch.empty(w.d, dtype=torch.double).pin_memory()
+hout = torch.empty(1 + w.d, dtype=torch.double).pin_memory()
+dout = torch.empty(1 + w.d, dtype=torch.double, device="cuda")
+dx = torch.empty(1, w.d, dtype=torch.double, device="cuda")
+for name, h2d, d2h in (("sync_only", False, False), ("h2d+sync", True, False), ("d2h+sync", False, True),
+                       ("h2d+d2h+sync", True, True)):
+    ts = []
+    for i in range(calls):
+        t0 = time.perf_counter()
+        if h2d:
+            dx.copy_(hx.view(1, w.d), non_blocking=True)
+            kg, g = p1.forward_grad(dx)
+        else:
+            kg, g = p1.forward_grad(xs[i])
+        if d2h:
+            hout.copy_(dout, non_blocking=True)
+        stream.synchronize()
+        ts.append(time.perf_counter() - t0)
+    res[name] = med(ts)
+# host overhead of the pieces alone
+ts = []
+for i in range(calls):
+    t0 = time.perf_counter()
+    torch.cuda.current_stream()
+    ts.append(time.perf_counter() - t0)
+res["current_stream_call"] = med(ts)
+ts = []
+for i in range(calls):
+    t0 = time.perf_counter()
+    with torch.cuda.device(0):
+        pass
+    ts.append(time.perf_counter() - t0)
+res["device_ctx"] = med(ts)
+ts = []
+for i in range(calls):
+    xa = xh[i].unsqueeze(-2).requires_grad_(True)
+    t0 = time.perf_counter()
+    loss = -acq(xa).sum()
+    (ga,) = torch.autograd.grad(loss, xa)
+    ts.append(time.perf_counter() - t0)
+res["autograd_route"] = med(ts)
+ts = []
+for i in range(calls):
+    t0 = time.perf_counter()
+    acq.value_and_grad_host(xh[i])
+    ts.append(time.perf_counter() - t0)
+res["value_and_grad_host"] = med(ts)
+
 ref = [p1.forward_grad(xs[i]) for i in range(8)]
 ref = [(a.cpu(), b.cpu()) for a, b in ref]
 if hasattr(p1, "forward_grad_host"):

@@ -1,6 +1,6 @@
 """Per-workgroup phase stamps of the value+gradient kernels (DKG_DEBUG_STAMPS=1).
 
-Run on the GPU box from the repo root:  python tools/kstamps_grad.py [workload]
+Run on the GPU box from the repo root:  python tools/kstamps_grad.py [workload] [B]
 Prints, for the last of 20 back-to-back headline forwards: each kernel's
 workgroup start/end window on the 100 MHz clock (relative to the first
 cross_root start, so the gaps between kernels show), and the per-phase
@@ -23,8 +23,9 @@ from dkg_amd.synthetic import WORKLOADS, make_problem  # noqa: E402
 w = WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "headline"]
 model, D, X, W = make_problem(w)
 acq = DiscreteKnowledgeGradient(model, D, W)
-plan = acq._plan_for(w.B, grad=True)
-Xd = X.cuda().contiguous()
+B = int(sys.argv[2]) if len(sys.argv) > 2 else w.B
+plan = acq._plan_for(B, grad=True)
+Xd = X[:B].cuda().contiguous()
 kg = torch.empty(w.B, dtype=torch.double, device="cuda")
 for _ in range(20):
     plan.forward_grad(Xd)
@@ -33,8 +34,6 @@ n = 3 * 1024 * 8
 buf = (ctypes.c_ulonglong * n)()
 _lib.check(_lib.load().dkg_debug_read_kstamps(buf, n), "kstamps")
 st = np.frombuffer(buf, dtype=np.uint64).reshape(3, 1024, 8).astype(np.int64)
-nwg = [(w.B + 15) // 16 * ((256 // 16 + 1) // 2) * w.m, ((D.shape[0] + 15) // 16) * ((w.B + 15) // 16) * w.m,
-       w.B * plan.state.m and None]
 names = ["cross_root", "posterior_cov", "envelope"]
 phases = {0: ["plan+prefetch", "stage X", "K fill", "MFMA", "reduce+store"],
           1: ["epi loads", "loads+MFMA", "LDS part", "reduce+store", "-"],
@@ -44,6 +43,9 @@ for k in range(3):
     s = st[k]
     used = s[:, 0] > 0
     s = s[used]
+    if not used.any():
+        print(f"{names[k]}: no stamps")
+        continue
     if t0 is None:
         t0 = s[:, 0].min()
     rt0, rt1 = (s[:, 0] - t0) / 100.0, (s[:, 7] - t0) / 100.0  # us
