@@ -65,6 +65,14 @@ __device__ __forceinline__ unsigned long long* kst_slot(int dst, const Plan* P, 
 constexpr int ENV_CAP = 128;
 constexpr int HCAP = 128;  // GRAD: queued envelope lines per wave before their gradient terms are flushed
 constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lines)
+// Streaming forward with LDS-staged chunks (M = 2..4): the extremes and filter passes read the line
+// records from LDS, STAGED_SLOTS * 64 lines per chunk, double-buffered and shared by the workgroup's pairs.
+constexpr int STAGED_SLOTS = 8;
+__host__ __device__ constexpr bool stream_staged(int M) { return M >= 2 && M <= 4; }
+// Doubles of one staged chunk array: the records of the chunk's STAGED_SLOTS * 64 lines, transposed into
+// rec / 2 planes of 16-byte component pairs (plane-major), so a lane's 16-byte reads are consecutive
+// across the wave (no LDS bank conflict); four arrays: (mu, cov) x 2 buffers.
+__host__ __device__ constexpr int staged_chunk_len(int rec) { return STAGED_SLOTS * 64 * rec; }
 // Streaming forward (no LDS staging): the survivor list holds up to
 // LIST_CAP_STREAM entries per wave; a list that does not fit the hull stage
 // (ENV_CAP - 3) is cut down by quickhull rounds (refine_list) instead of the
@@ -929,79 +937,97 @@ __device__ __forceinline__ int refine_stream(const FwdEnv& f, int nch, int nl, i
 // extremes in one lexicographic pass over the streamed lines, the margin
 // filter into the wave's long list (LIST_CAP_STREAM entries), streamed
 // quickhull rounds when that overflows, then the walk over the list.
-template <int MAXL, class Build>
-__device__ __forceinline__ FwdEnv env_extremes_stream(int nch, int nl, int lane, Build&& build) {
-  FwdEnv f;
+// Per-lane running extremes of streamed lines (L = min b, tie max a; R = max b, tie max a; T = max a,
+// tie min b), folded chunk by chunk and reduced over the wave once (env_extremes_stream).
+struct ExtAcc {
   double bmin = INFINITY, aLx = -INFINITY, bmax = -INFINITY, aRx = -INFINITY, amax = -INFINITY, bTx = INFINITY;
-  for (int c = 0; c < nch; ++c) {
-    double la[MAXL], lb[MAXL];
-    build(c, la, lb);
+};
+
+template <int MAXL>
+__device__ __forceinline__ void ext_fold(const double (&la)[MAXL], const double (&lb)[MAXL], int base, int nl, int lane,
+                                         ExtAcc& e) {
 #pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      const bool live = c * 64 * MAXL + lane + 64 * t < nl;
-      const double a = la[t], b = lb[t];
-      const bool l = live && (b < bmin || (b == bmin && a > aLx));
-      bmin = l ? b : bmin;
-      aLx = l ? a : aLx;
-      const bool r = live && (b > bmax || (b == bmax && a > aRx));
-      bmax = r ? b : bmax;
-      aRx = r ? a : aRx;
-      const bool tt = live && (a > amax || (a == amax && b < bTx));
-      amax = tt ? a : amax;
-      bTx = tt ? b : bTx;
-    }
+  for (int t = 0; t < MAXL; ++t) {
+    // bitwise, not short-circuit, logic: lane masks and selects, no branch per slot
+    const bool live = base + lane + 64 * t < nl;
+    const double a = la[t], b = lb[t];
+    const bool l = live & ((b < e.bmin) | ((b == e.bmin) & (a > e.aLx)));
+    e.bmin = l ? b : e.bmin;
+    e.aLx = l ? a : e.aLx;
+    const bool r = live & ((b > e.bmax) | ((b == e.bmax) & (a > e.aRx)));
+    e.bmax = r ? b : e.bmax;
+    e.aRx = r ? a : e.aRx;
+    const bool tt = live & ((a > e.amax) | ((a == e.amax) & (b < e.bTx)));
+    e.amax = tt ? a : e.amax;
+    e.bTx = tt ? b : e.bTx;
   }
+}
+
+__device__ __forceinline__ FwdEnv ext_reduce(ExtAcc e) {
   DKG_BUTTERFLY({
-    const double ob = partner_f64<S_>(bmin), oa = partner_f64<S_>(aLx);
-    const bool l = ob < bmin || (ob == bmin && oa > aLx);
-    bmin = l ? ob : bmin;
-    aLx = l ? oa : aLx;
-    const double ob2 = partner_f64<S_>(bmax), oa2 = partner_f64<S_>(aRx);
-    const bool r = ob2 > bmax || (ob2 == bmax && oa2 > aRx);
-    bmax = r ? ob2 : bmax;
-    aRx = r ? oa2 : aRx;
-    const double oa3 = partner_f64<S_>(amax), ob3 = partner_f64<S_>(bTx);
-    const bool tt = oa3 > amax || (oa3 == amax && ob3 < bTx);
-    amax = tt ? oa3 : amax;
-    bTx = tt ? ob3 : bTx;
+    const double ob = partner_f64<S_>(e.bmin), oa = partner_f64<S_>(e.aLx);
+    const bool l = ob < e.bmin || (ob == e.bmin && oa > e.aLx);
+    e.bmin = l ? ob : e.bmin;
+    e.aLx = l ? oa : e.aLx;
+    const double ob2 = partner_f64<S_>(e.bmax), oa2 = partner_f64<S_>(e.aRx);
+    const bool r = ob2 > e.bmax || (ob2 == e.bmax && oa2 > e.aRx);
+    e.bmax = r ? ob2 : e.bmax;
+    e.aRx = r ? oa2 : e.aRx;
+    const double oa3 = partner_f64<S_>(e.amax), ob3 = partner_f64<S_>(e.bTx);
+    const bool tt = oa3 > e.amax || (oa3 == e.amax && ob3 < e.bTx);
+    e.amax = tt ? oa3 : e.amax;
+    e.bTx = tt ? ob3 : e.bTx;
   })
-  f.bL = bmin; f.aL = aLx; f.bR = bmax; f.aR = aRx; f.aT = amax; f.bT = bTx;
+  FwdEnv f;
+  f.bL = e.bmin; f.aL = e.aLx; f.bR = e.bmax; f.aR = e.aRx; f.aT = e.amax; f.bT = e.bTx;
   f.cnt = 0;
-  f.status = uniform(fmax(fabs(bmin), fabs(bmax)) >= 1e-9 && bmin < bmax) ? 0 : 1;
+  f.status = uniform(fmax(fabs(e.bmin), fabs(e.bmax)) >= 1e-9 && e.bmin < e.bmax) ? 0 : 1;
   return f;
 }
 
 template <int MAXL, class Build>
-__device__ __forceinline__ EdgeSum env_pair_stream_edges(int nch, int nl, int lane, double* sb, double* sa, int* si,
-                                                  double* vreg, bool force_walk, int* nhull, Build&& build) {
-  const FwdEnv f = env_extremes_stream<MAXL>(nch, nl, lane, build);
-  if (f.status == 1) {
-    *nhull = 1;
-    return EdgeSum{0.0, 0.0, 0.0, false};
-  }
-  const EnvChords ch = env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR);
-  int cnt = 0;
+__device__ __forceinline__ FwdEnv env_extremes_stream(int nch, int nl, int lane, Build&& build) {
+  ExtAcc e;
   for (int c = 0; c < nch; ++c) {
     double la[MAXL], lb[MAXL];
     build(c, la, lb);
+    ext_fold<MAXL>(la, lb, c * 64 * MAXL, nl, lane, e);
+  }
+  return ext_reduce(e);
+}
+
+// The chord filter of one streamed chunk (lines base + lane + 64 t) into the wave's long list
+// (LIST_CAP_STREAM entries; cnt counts on past it).
+template <int MAXL>
+__device__ __forceinline__ void stream_keep(const double (&la)[MAXL], const double (&lb)[MAXL], int base, int nl,
+                                            const EnvChords& ch, int lane, double* sb, double* sa, int* si,
+                                            int& cnt) {
 #pragma unroll
-    for (int t = 0; t < MAXL; ++t) {
-      const int k = c * 64 * MAXL + lane + 64 * t;
-      const bool s = k < nl && env_keep(ch, la[t], lb[t]);
-      const uint64_t mk = ballot(s);
-      if (mk != 0) {
-        if (s) {
-          const int pos = cnt + lanes_below(mk);
-          if (pos < LIST_CAP_STREAM) {
-            sb[pos] = lb[t];
-            sa[pos] = la[t];
-            si[pos] = k;
-          }
+  for (int t = 0; t < MAXL; ++t) {
+    const int k = base + lane + 64 * t;
+    // env_keep with bitwise logic: lane masks, no branch per slot
+    const bool s = (k < nl) & ((fma(-ch.s1, lb[t], la[t]) >= ch.k1) | (fma(-ch.s2, lb[t], la[t]) >= ch.k2));
+    const uint64_t mk = ballot(s);
+    if (mk != 0) {
+      if (s) {
+        const int pos = cnt + lanes_below(mk);
+        if (pos < LIST_CAP_STREAM) {
+          sb[pos] = lb[t];
+          sa[pos] = la[t];
+          si[pos] = k;
         }
-        cnt += __popcll(mk);
       }
+      cnt += __popcll(mk);
     }
   }
+}
+
+// After the extremes and the filter pass (cnt survivors in the list): quickhull rounds if the list
+// overflowed, the list walk, and the walk over all streamed lines when neither settles the pair.
+template <int MAXL, class Build>
+__device__ __forceinline__ EdgeSum env_pair_stream_tail(const FwdEnv& f, int cnt, int nch, int nl, int lane,
+                                                        double* sb, double* sa, int* si, double* vreg,
+                                                        bool force_walk, int* nhull, Build&& build) {
   if (cnt > LIST_CAP_STREAM && !force_walk) cnt = refine_stream<MAXL>(f, nch, nl, lane, sb, sa, si, vreg, build);
   if (cnt >= 0 && cnt <= LIST_CAP_STREAM && !force_walk) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1019,6 +1045,24 @@ __device__ __forceinline__ EdgeSum env_pair_stream_edges(int nch, int nl, int la
     }
   }
   return walk_stream<MAXL>(nch, nl, lane, f.bL, f.aL, f.bT, nhull, build);
+}
+
+template <int MAXL, class Build>
+__device__ __forceinline__ EdgeSum env_pair_stream_edges(int nch, int nl, int lane, double* sb, double* sa, int* si,
+                                                  double* vreg, bool force_walk, int* nhull, Build&& build) {
+  const FwdEnv f = env_extremes_stream<MAXL>(nch, nl, lane, build);
+  if (f.status == 1) {
+    *nhull = 1;
+    return EdgeSum{0.0, 0.0, 0.0, false};
+  }
+  const EnvChords ch = env_chords(f.bL, f.aL, f.bT, f.aT, f.bR, f.aR);
+  int cnt = 0;
+  for (int c = 0; c < nch; ++c) {
+    double la[MAXL], lb[MAXL];
+    build(c, la, lb);
+    stream_keep<MAXL>(la, lb, c * 64 * MAXL, nl, ch, lane, sb, sa, si, cnt);
+  }
+  return env_pair_stream_tail<MAXL>(f, cnt, nch, nl, lane, sb, sa, si, vreg, force_walk, nhull, build);
 }
 
 template <int MAXL, class Build>
@@ -1323,9 +1367,15 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   double* sb = sbuf + (size_t)wave * 2 * LC;
   double* sa = sb + LC;
   // streaming forward: the quickhull refinement's vertex arrays after the lists
-  double* vreg = sbuf + (size_t)SW * 2 * LC + (size_t)wave * VREG;
+  // staged streaming forward: the chunk buffers take the vertex arrays' place (the refinement runs
+  // after the staged passes, so it reuses their room)
+  constexpr bool STG = STREAM && !GRAD && stream_staged(M);
+  constexpr int CBL = STG ? staged_chunk_len(cov_rec(M)) : 0;
+  const int vreg_room = STG ? max(SW * VREG, 4 * CBL) : ((STREAM && !GRAD) ? SW * VREG : 0);
+  double* cbuf = sbuf + (size_t)SW * 2 * LC;
+  double* vreg = cbuf + (size_t)wave * VREG;
   // forward: the list's line indices after the vertex arrays (GRAD: sidx)
-  int* sif = reinterpret_cast<int*>(sbuf + (size_t)SW * (2 * LC + ((STREAM && !GRAD) ? VREG : 0))) +
+  int* sif = reinterpret_cast<int*>(sbuf + (size_t)SW * 2 * LC + vreg_room) +
              (size_t)wave * LC;
   int* si = nullptr;
   double* gw = nullptr;
@@ -1358,6 +1408,149 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     sv[i] = sgpr_f64(live ? s_pp[i * 6 + 4] : 0.0);
     mx0[i] = sgpr_f64(live ? s_pp[i * 6 + 5] : 0.0);
   }
+
+  // ---- staged streaming forward: the extremes pass and the filter pass of every pair of the workgroup
+  // over LDS-staged chunks of the line records (chunk q: lines q*SCH .. q*SCH + SCH - 1, records k - 1),
+  // the next chunk's DMA in flight while the current one is read; the survivor lists then go to the
+  // per-pair tail (refinement, walks) below.  Waves without a pair stage with the others.
+  FwdEnv sf;
+  int scnt = 0;
+  if constexpr (STG) {
+    constexpr int CS = STAGED_SLOTS, SCH = 64 * CS;
+    const int lane = lane_k;
+    const bool has = j0 + wave < j1;
+    const int jj = has ? j0 + wave : j0;
+    double w[M], wa[M], wb[M];
+    double a_off, den;
+    pair_coefs<M>(lw + jj * m, m, full, target, ysd, ymu, nz, sv, w, wa, wb, a_off, den);
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      wa[i] = sgpr_f64(wa[i]);
+      wb[i] = sgpr_f64(wb[i]);
+    }
+    a_off = sgpr_f64(a_off);
+    double bb0 = 0.0, a0 = a_off, wbt = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      bb0 = fma(wb[i], sv[i], bb0);
+      a0 = fma(wa[i], mx0[i], a0);
+      wbt = (i == target) ? wb[i] : wbt;
+    }
+    const int nq = (NL + SCH - 1) / SCH;
+    const double* cvb = cov_all + (size_t)b * cov_stride;
+    // chunk q's records into buffer q & 1 by a transposing DMA: position p of plane q2 holds component
+    // pair q2 of record q*SCH - 1 + p (line q*SCH + p; clamped into 0 .. N-1, the clamped positions are
+    // line 0, built from registers, and padding lines); one instruction = 64 positions of one plane
+    auto stage = [&](int q) {
+      constexpr int NP2 = MP / 2, GR = SCH / 64, NI = NP2 * GR;
+      double* bm = cbuf + (size_t)(q & 1) * 2 * CBL;
+      for (int ii = wave; ii < 2 * NI; ii += SW) {
+        const int arr = ii / NI, rem = ii % NI, q2 = rem / GR, gi = rem % GR;
+        const double* src = arr ? cvb : mu_all;
+        const int rec = min(max(q * SCH - 1 + gi * 64 + lane_k, 0), N - 1);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (size_t)rec * MP + 2 * q2),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(bm + (size_t)arr * CBL +
+                                                                         ((size_t)q2 * SCH + gi * 64) * 2)),
+                                         16, 0, 0);
+      }
+    };
+    // build_chunk's lines (same arithmetic, same order) from the staged records of chunk q
+    auto build_staged = [&](int q, double (&la)[CS], double (&lb)[CS]) {
+      const double* bm = cbuf + (size_t)(q & 1) * 2 * CBL;
+      const double* mur = bm + lane * 2;        // plane q2, slot t: + (q2 * SCH + 64 t) * 2
+      const double* cvr = bm + CBL + lane * 2;
+      const int kbase = q * SCH;
+      // 16-byte reads, consecutive across the wave; components i >= m carry zero weights over zero
+      // padding, so the sums are build_chunk's.  The full / target choice outside the slot loop: one LDS
+      // read stream, no wait per slot.
+      auto adot = [&](const double* r, const double (&c)[M], double acc) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q2 = 0; 2 * q2 < M; ++q2) {
+          const double2 u = *reinterpret_cast<const double2*>(r + (size_t)q2 * SCH * 2);
+          acc = fma(c[2 * q2], u.x, acc);
+          if (2 * q2 + 1 < M) acc = fma(c[2 * q2 + 1], u.y, acc);
+        }
+        return acc;
+      };
+      const int tg = full ? 0 : target;
+      const double* cvt = cvr + (size_t)(tg >> 1) * SCH * 2 + (tg & 1);  // target path
+      if (full) {
+#pragma unroll
+        for (int t = 0; t < CS; ++t) {
+          la[t] = adot(mur + 128 * t, wa, a_off);
+          lb[t] = adot(cvr + 128 * t, wb, 0.0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < CS; ++t) {
+          la[t] = adot(mur + 128 * t, wa, a_off);
+          lb[t] = fma(wbt, cvt[128 * t], 0.0);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < CS; ++t) {
+        if (kbase + 64 * t + 63 > N) {  // wave-uniform: padding lines in this slot
+          const bool pad = kbase + lane + 64 * t > N;
+          la[t] = pad ? -INFINITY : la[t];
+          lb[t] = pad ? bb0 : lb[t];
+        }
+      }
+      if (q == 0) {
+        la[0] = (lane == 0) ? a0 : la[0];
+        lb[0] = (lane == 0) ? bb0 : lb[0];
+      }
+    };
+    // pass 1: extremes
+    ExtAcc e;
+#ifdef DKG_STG_STAMPS
+    unsigned long long twait = 0, tw0 = 0;
+#define STG_W0 tw0 = __builtin_amdgcn_s_memtime();
+#define STG_W1 twait += __builtin_amdgcn_s_memtime() - tw0;
+#else
+#define STG_W0
+#define STG_W1
+#endif
+    stage(0);
+    for (int q = 0; q < nq; ++q) {
+      STG_W0
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // chunk q landed; every wave is done with the other buffer
+      STG_W1
+      if (q + 1 < nq) stage(q + 1);
+      if (has) {
+        double la[CS], lb[CS];
+        build_staged(q, la, lb);
+        ext_fold<CS>(la, lb, q * SCH, NL, lane, e);
+      }
+    }
+    sf = ext_reduce(e);
+    // pass 2: the chord filter into the survivor list
+    const bool live = has && sf.status == 0;
+    const EnvChords ch = env_chords(sf.bL, sf.aL, sf.bT, sf.aT, sf.bR, sf.aR);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is done with the last chunk of pass 1
+    stage(0);
+    for (int q = 0; q < nq; ++q) {
+      STG_W0
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      STG_W1
+      if (q + 1 < nq) stage(q + 1);
+      if (live) {
+        double la[CS], lb[CS];
+        build_staged(q, la, lb);
+        stream_keep<CS>(la, lb, q * SCH, NL, ch, lane, sb, sa, sif, scnt);
+      }
+    }
+    __syncthreads();  // the chunk buffers are the refinement's vertex arrays from here
+#ifdef DKG_STG_STAMPS
+    if (st) st[4] = twait;  // raw: wait cycles of wave 0 over both passes
+    if (st) st[5] = __builtin_amdgcn_s_memtime();
+#endif
+  }
+#undef STG_W0
+#undef STG_W1
 
   if (const int j = j0 + wave; j < j1) {
     const int lane = lane_k;
@@ -1738,6 +1931,14 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
       }
       if (lane == 0)
         for (int dd = 0; dd < d; ++dd) gw[dd] = 0.0;
+    } else if constexpr (STG) {
+      if (sf.status == 1) {
+        kgj = 0.0;
+        hn = 1;
+      } else {
+        kgj = finish_edges(env_pair_stream_tail<MAXL>(sf, scnt, nch, NL, lane, sb, sa, sif, vreg, force_walk, &hn,
+                                                      build_chunk));
+      }
     } else if constexpr (STREAM) {
       kgj = env_pair_stream<MAXL>(nch, NL, lane, sb, sa, sif, vreg, force_walk, &hn, build_chunk);
     } else {
@@ -1758,9 +1959,13 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   }
 
   // ---- mean over S: per-wave sums -> per-WG sum (fixed order) -> across WGs
+#ifndef DKG_STG_STAMPS
   if (!GRAD) KST(st, 4);
+#endif
   __syncthreads();
+#ifndef DKG_STG_STAMPS
   if (!GRAD) KST(st, 5);
+#endif
   if constexpr (GRAD) {
     if (threadIdx.x < d) {
       double gs = 0.0;

@@ -154,7 +154,11 @@ size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad
   const bool refine = stream && !grad;  // streaming forward: long lists + quickhull vertex arrays
   const size_t lc = list_cap(refine);
   // per wave: the list (slopes, intercepts; forward: line indices) and the streaming vertex arrays
-  return ((size_t)2 + staged + ((S * m + 1) & ~1) + ((S + 1) & ~1) + (size_t)waves * 2 * lc + (refine ? (size_t)waves * VREG : 0) +
+  // streaming forward: the quickhull vertex arrays, or (M = 2..4) the staged chunk buffers in their place
+  const size_t vroom = !refine ? 0
+                       : stream_staged(M) ? std::max((size_t)waves * VREG, (size_t)4 * staged_chunk_len(cov_rec(M)))
+                                          : (size_t)waves * VREG;
+  return ((size_t)2 + staged + ((S * m + 1) & ~1) + ((S + 1) & ~1) + (size_t)waves * 2 * lc + vroom +
           (grad ? 0 : ((size_t)waves * lc + 1) / 2)) * sizeof(double);
 }
 
