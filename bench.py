@@ -515,7 +515,7 @@ def main():
                 xa = x1.unsqueeze(-2).requires_grad_(True)
                 loss = -acq(xa).sum()
                 (ga,) = torch.autograd.grad(loss, xa)
-                float(loss), ga.numpy()
+                float(loss.detach()), ga.numpy()
                 ta.append(time.perf_counter() - t0)
             ts.sort()
             te.sort()

@@ -3,7 +3,8 @@ import json
 import sys
 
 for f in sys.argv[1:]:
-    d = json.load(open(f))
+    # the last JSON line of the file (gloo and torchrun may print other lines to stdout)
+    d = json.loads([ln for ln in open(f) if ln.startswith("{")][-1])
     nd = d.get("nondegenerate") or {}
     st = d.get("stress") or {}
     b1 = d.get("latency_b1") or {}

@@ -1,6 +1,6 @@
 """Worst parity ratios of the HIP forward against the oracle (GPU box, repo root).
 
-usage: python tools/parity_report.py [out.json]   (default profiles/r02_parity.json)
+usage: python tools/parity_report.py [out.json]   (default profiles/r03_parity.json)
 
 For every workload and path, tests/helpers.parity_case on the same candidates the GPU parity
 tests use: the device lines against oracle.lines_batched (relative gap), the envelope kernel on
@@ -19,11 +19,11 @@ sys.path[:0] = [REPO, os.path.join(REPO, "decoupled-kg_amd"), os.path.join(REPO,
 from dkg_amd.synthetic import WORKLOADS, make_problem  # noqa: E402
 from helpers import LINE_RTOL, parity_case  # noqa: E402
 
-CASES = [("small", 32), ("parity6d", 32), ("headline", 128), ("headline_nd", 128), ("stress", 4)]
+CASES = [("small", 32), ("parity6d", 32), ("headline", 128), ("headline_nd", 128), ("stress", 64)]
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r02_parity.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r03_parity.json")
     rep = {"line_rtol": LINE_RTOL, "cases": []}
     for wname, nX in CASES:
         model, D, X, W = make_problem(WORKLOADS[wname])
