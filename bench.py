@@ -90,6 +90,7 @@ def parse():
     ap.add_argument("--pmc", default="auto",
                     help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py); auto: "
                          "profiles/r03/pmc_<workload>[_fp32].json, none if that file does not exist")
+    ap.add_argument("--prep-reps", type=int, default=5, help="timed device-state preparations (0 = skip)")
     ap.add_argument("--stress-steps", type=int, default=8,
                     help="timed forwards of the stress leg (BASELINE configs[4] shape, fp64; 0 = skip)")
     return ap.parse_args()
@@ -531,6 +532,24 @@ def main():
                               "pinned D2H), device round trip included; eager_two_copies: the plan's C call on a "
                               "device candidate + two .cpu() copies"}
 
+    # ---- state preparation: what a refit costs before the first forward (DeviceGPState: per output the
+    # kernel matrix, Cholesky with the psd_safe_cholesky jitter check, the inverse, alpha, Q_D and mu_D)
+    prep = None
+    if args.prep_reps > 0:
+        from dkg_amd.gp_state import DeviceGPState
+
+        DeviceGPState(model, D, dev)
+        torch.cuda.synchronize()
+        tp_ = []
+        for _ in range(args.prep_reps):
+            t0 = time.perf_counter()
+            DeviceGPState(model, D, dev)
+            torch.cuda.synchronize()
+            tp_.append(time.perf_counter() - t0)
+        tp_.sort()
+        prep = {"ms_median": tp_[len(tp_) // 2] * 1e3, "ms_min": tp_[0] * 1e3, "outputs": w.m, "reps": len(tp_),
+                "what": "DeviceGPState(model, D) on the host clock, synchronised: every output's caches"}
+
     # ---- non-degenerate leg: headline sizes, KG > 0 for every pair (workload headline_nd, d = 6)
     nd = None
     if args.nd_steps > 0 and args.workload == "headline" and args.precision == "fp64":
@@ -592,6 +611,7 @@ def main():
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
             "latency_b1": lat_b1,
+            "state_prep": prep,
             "roofline": roof,
             "forward_roofline": fwd_roof,
             "batch_stats": stats,

@@ -323,8 +323,9 @@ size_t dkg_prepare_workspace(int n) {
   return align256((size_t)n * n * sizeof(double)) + 256;
 }
 
-int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int max_tries, double* L, void* work,
-                       size_t work_bytes, double* alpha, double* root_frag, double* jitter_used, void* stream) {
+// Argument checks of one output's preparation (dkg_prepare_output / dkg_prepare_outputs).
+static int check_prepare(const dkg_output* o, int d, const double* train_y, int max_tries, const double* L,
+                         const void* work, size_t work_bytes, const double* alpha, const double* root_frag) {
   if (!o || !train_y || !L || !work || !alpha || !root_frag || !o->inv_lengthscale || !o->train_x)
     return fail(DKG_ERR_ARG, "NULL pointer");
   const int n = o->n;
@@ -335,32 +336,94 @@ int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int ma
   if (max_tries < 0) return fail(DKG_ERR_ARG, "max_tries=%d", max_tries);
   if (work_bytes < dkg_prepare_workspace(n))
     return fail(DKG_ERR_WORKSPACE, "workspace %zu bytes < required %zu", work_bytes, dkg_prepare_workspace(n));
-  hipStream_t s = (hipStream_t)stream;
-  double* X = static_cast<double*>(work);
-  int* info = reinterpret_cast<int*>(static_cast<char*>(work) + align256((size_t)n * n * sizeof(double)));
+  return DKG_OK;
+}
+
+static int* prepare_info(void* work, int n) {
+  return reinterpret_cast<int*>(static_cast<char*>(work) + align256((size_t)n * n * sizeof(double)));
+}
+
+// psd_safe_cholesky's attempts first .. max_tries of one output (attempt 0: no jitter; then absolute jitter
+// 1e-8 * 10^(attempt - 1)), each checked on the host.  *jit: the jitter that worked.
+static int cholesky_attempts(const dkg_output* o, int d, double* L, int* info, int first, int max_tries, hipStream_t s,
+                             double* jit) {
   int st, h_info = 1;
-  double jit = 0.0;
-  for (int attempt = 0; attempt <= max_tries; ++attempt) {
-    // linear_operator psd_safe_cholesky: plain first, then absolute jitter 1e-8 * 10^i
-    jit = attempt == 0 ? 0.0 : 1e-8 * std::pow(10.0, attempt - 1);
-    if ((st = hip_check(launch_kernel_matrix(*o, d, o->train_x, n, o->train_x, n, o->noise + jit, L, s),
+  for (int attempt = first; attempt <= max_tries; ++attempt) {
+    *jit = attempt == 0 ? 0.0 : 1e-8 * std::pow(10.0, attempt - 1);
+    if ((st = hip_check(launch_kernel_matrix(*o, d, o->train_x, o->n, o->train_x, o->n, o->noise + *jit, L, s),
                         "kernel_matrix")))
       return st;
     if ((st = hip_check(hipMemsetAsync(info, 0, sizeof(int), s), "hipMemsetAsync")) ||
-        (st = hip_check(launch_cholesky(L, n, info, s), "cholesky")) ||
+        (st = hip_check(launch_cholesky(L, o->n, info, s), "cholesky")) ||
         (st = hip_check(hipMemcpyAsync(&h_info, info, sizeof(int), hipMemcpyDeviceToHost, s), "hipMemcpyAsync")) ||
         (st = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize")))
       return st;
-    if (h_info == 0) break;
+    if (h_info == 0) return DKG_OK;
   }
-  if (h_info != 0)
-    return fail(DKG_ERR_NOT_PD, "covariance not positive definite after %d jitter retries (pivot %d)", max_tries,
-                h_info);
+  return fail(DKG_ERR_NOT_PD, "covariance not positive definite after %d jitter retries (pivot %d)", max_tries,
+              h_info);
+}
+
+int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int max_tries, double* L, void* work,
+                       size_t work_bytes, double* alpha, double* root_frag, double* jitter_used, void* stream) {
+  int st = check_prepare(o, d, train_y, max_tries, L, work, work_bytes, alpha, root_frag);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int n = o->n;
+  double* X = static_cast<double*>(work);
+  int* info = prepare_info(work, n);
+  double jit = 0.0;
+  if ((st = cholesky_attempts(o, d, L, info, 0, max_tries, s, &jit))) return st;
   if (jitter_used) *jitter_used = jit;
   if ((st = hip_check(launch_tri_inverse(L, X, n, info, s), "tri_inverse")) ||
       (st = hip_check(launch_alpha(X, train_y, o->mean_constant, n, alpha, info, s), "alpha")) ||
       (st = hip_check(launch_pack_linv(X, n, root_frag, s), "pack_linv")))
     return st;
+  return DKG_OK;
+}
+
+int dkg_prepare_outputs(const dkg_output* outs, int m, int d, const double* const* train_y, int max_tries,
+                        double* const* L, void* const* work, const size_t* work_bytes, double* const* alpha,
+                        double* const* root_frag, double* jitter_used, void* stream) {
+  if (!outs || m < 1 || m > DKG_MAX_OUTPUTS) return fail(DKG_ERR_ARG, "m=%d outputs (1..%d)", m, DKG_MAX_OUTPUTS);
+  if (!train_y || !L || !work || !work_bytes || !alpha || !root_frag) return fail(DKG_ERR_ARG, "NULL pointer");
+  int st;
+  for (int i = 0; i < m; ++i)
+    if ((st = check_prepare(&outs[i], d, train_y[i], max_tries, L[i], work[i], work_bytes[i], alpha[i], root_frag[i])))
+      return st;
+  hipStream_t s = (hipStream_t)stream;
+  PrepBatch b{};
+  int h_info[DKG_MAX_OUTPUTS];
+  double jit[DKG_MAX_OUTPUTS];
+  for (int i = 0; i < m; ++i) {
+    b.A[i] = L[i];
+    b.X[i] = static_cast<double*>(work[i]);
+    b.n[i] = outs[i].n;
+    b.info[i] = prepare_info(work[i], outs[i].n);
+    jit[i] = 0.0;
+    if ((st = hip_check(launch_kernel_matrix(outs[i], d, outs[i].train_x, outs[i].n, outs[i].train_x, outs[i].n,
+                                             outs[i].noise, L[i], s), "kernel_matrix")) ||
+        (st = hip_check(hipMemsetAsync(b.info[i], 0, sizeof(int), s), "hipMemsetAsync")))
+      return st;
+  }
+  // every output's first attempt in one chain of launches, one status check for all
+  if ((st = hip_check(launch_cholesky_batch(b, m, s), "cholesky_batch"))) return st;
+  for (int i = 0; i < m; ++i)
+    if ((st = hip_check(hipMemcpyAsync(&h_info[i], b.info[i], sizeof(int), hipMemcpyDeviceToHost, s),
+                        "hipMemcpyAsync")))
+      return st;
+  if ((st = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return st;
+  for (int i = 0; i < m; ++i)  // the outputs that need jitter are retried on their own, as dkg_prepare_output
+    if (h_info[i] != 0 && (st = cholesky_attempts(&outs[i], d, L[i], b.info[i], 1, max_tries, s, &jit[i])))
+      return st;
+  if ((st = hip_check(launch_tri_inverse_batch(b, m, s), "tri_inverse_batch"))) return st;
+  for (int i = 0; i < m; ++i) {
+    if ((st = hip_check(launch_alpha(b.X[i], train_y[i], outs[i].mean_constant, outs[i].n, alpha[i], b.info[i], s),
+                        "alpha")) ||
+        (st = hip_check(launch_pack_linv(b.X[i], outs[i].n, root_frag[i], s), "pack_linv")))
+      return st;
+    if (jitter_used) jitter_used[i] = jit[i];
+  }
   return DKG_OK;
 }
 

@@ -76,6 +76,16 @@ hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
 // State preparation (dkg_linalg.hip): blocked Cholesky with device status,
 // triangular inverse, alpha = Linv^T Linv (y - c), root_frag from Linv.
 hipError_t launch_cholesky(double* A, int n, int* info, hipStream_t s);
+// Several outputs' factorisations side by side: every launch of the blocked chains carries all of them
+// (blockIdx.y / z = output).  A = the matrix (Cholesky) or L (inverse), X = the inverse's output.
+struct PrepBatch {
+  double* A[DKG_MAX_OUTPUTS];
+  double* X[DKG_MAX_OUTPUTS];
+  int n[DKG_MAX_OUTPUTS];
+  int* info[DKG_MAX_OUTPUTS];
+};
+hipError_t launch_cholesky_batch(const PrepBatch& b, int m, hipStream_t s);
+hipError_t launch_tri_inverse_batch(const PrepBatch& b, int m, hipStream_t s);
 hipError_t launch_tri_inverse(double* L, double* X, int n, const int* info, hipStream_t s);
 hipError_t launch_alpha(const double* X, const double* y, double c, int n, double* alpha, const int* info,
                         hipStream_t s);

@@ -22,36 +22,45 @@ constexpr int LB = 32;  // block width
 // solve the rows below it, A[i, k0:k0+nb] <- A[i, k0:k0+nb] Lkk^{-T}.
 // info (device): 0 = fine; j + 1 = the pivot of column j is not positive/finite
 // (LAPACK potrf convention, what cholesky_ex reports).
-__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int n, int k0, int* __restrict__ info) {
+__device__ __forceinline__ void chol_panel_body(double* __restrict__ A, int n, int k0, int* __restrict__ info) {
   __shared__ double Lk[LB][LB + 1];
   __shared__ int bad;
   if (*info != 0) return;  // an earlier panel failed: nothing more to do
   const int nb = min(LB, n - k0);
   const int tid = threadIdx.x;
-  if (tid == 0) bad = 0;
-  for (int e = tid; e < LB * LB; e += blockDim.x) {
-    const int r = e / LB, c = e % LB;
-    Lk[r][c] = (r < nb && c <= r) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
-  }
-  __syncthreads();
-  // unblocked right-looking on the diagonal block
-  for (int j = 0; j < nb; ++j) {
-    const double piv = Lk[j][j];
-    __syncthreads();
-    if (!(piv > 0.0) || !isfinite(piv)) {  // NaN fails too
-      if (tid == 0 && bad == 0) bad = k0 + j + 1;
-      break;
+  if (tid < 64) {
+    // the diagonal block on one wave, in registers: lane r holds row r (zero rows past nb); column j's
+    // pivot and entries reach the other lanes by v_readlane, so the 32 steps need no LDS round trip
+    // and no barrier (the LDS version spent ~0.7 us per step on three barriers)
+    const int lane = tid;
+    double a[LB];
+#pragma unroll
+    for (int c = 0; c < LB; ++c) a[c] = (lane < nb && c <= lane) ? A[(size_t)(k0 + lane) * n + k0 + c] : 0.0;
+    int fail = 0;
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      if (j < nb && fail == 0) {  // uniform
+        const double piv = readlane_f64(a[j], j);
+        if (!(piv > 0.0) || !isfinite(piv)) {  // NaN fails too
+          fail = k0 + j + 1;
+        } else {
+          const double dj = sqrt(piv);
+          a[j] = (lane == j) ? dj : ((lane > j) ? a[j] / dj : a[j]);
+#pragma unroll
+          for (int c = j + 1; c < LB; ++c) {
+            if (c < nb) {
+              const double lcj = readlane_f64(a[j], c);  // L[c][j]
+              a[c] = (lane >= c) ? fma(-a[j], lcj, a[c]) : a[c];
+            }
+          }
+        }
+      }
     }
-    const double dj = sqrt(piv);
-    for (int r = j + 1 + tid; r < nb; r += blockDim.x) Lk[r][j] /= dj;
-    if (tid == 0) Lk[j][j] = dj;
-    __syncthreads();
-    const int m = nb - j - 1;
-    for (int e = tid; e < m * m; e += blockDim.x) {
-      const int r = j + 1 + e / m, c = j + 1 + e % m;
-      if (c <= r) Lk[r][c] -= Lk[r][j] * Lk[c][j];
+    if (lane < LB) {
+#pragma unroll
+      for (int c = 0; c < LB; ++c) Lk[lane][c] = a[c];
     }
-    __syncthreads();
+    if (lane == 0) bad = fail;
   }
   __syncthreads();
   if (bad != 0) {
@@ -76,11 +85,24 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
         for (int q = 0; q < c; ++q) s -= x[q] * Lk[c][q];
         x[c] = s / Lk[c][c];
       }
+      // no LDS read of a later row is hoisted above this one: the unrolled solve would otherwise keep
+      // all 528 Lk values live at once (256 VGPRs and ~700 bytes of scratch per lane)
+      asm volatile("" ::: "memory");
     }
 #pragma unroll
     for (int c = 0; c < LB; ++c)
       if (c < nb) row[c] = x[c];
   }
+}
+
+__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int n, int k0, int* __restrict__ info) {
+  chol_panel_body(A, n, k0, info);
+}
+
+// All outputs' panels at block column k0 in one launch (blockIdx.y = output; outputs with n <= k0 are done).
+__global__ __launch_bounds__(256) void chol_panel_batch_kernel(PrepBatch b, int k0) {
+  const int i = blockIdx.y;
+  if (k0 < b.n[i]) chol_panel_body(b.A[i], b.n[i], k0, b.info[i]);
 }
 
 // 32 x 32 tile update C -= P Q^T with P = A[pi.., kc..kc+32), Q = A[qi.., kc..kc+32)
@@ -113,12 +135,11 @@ __device__ __forceinline__ void tile_update(double* __restrict__ A, const double
 
 // Trailing update after panel k0: A[i][j] -= sum_c L[i][c] L[j][c] over the
 // panel's columns, for the lower tiles (ti >= tj) of the trailing matrix.
-__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int n, int k0,
-                                                          const int* __restrict__ info) {
+__device__ __forceinline__ void chol_update_body(double* __restrict__ A, int n, int k0, const int* __restrict__ info,
+                                                 int t) {
   if (*info != 0) return;
   const int base = k0 + LB;
-  // blockIdx.x enumerates lower tiles (ti, tj), tj <= ti, row-major over ti
-  const int t = blockIdx.x;
+  // t enumerates lower tiles (ti, tj), tj <= ti, row-major over ti
   int ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   while (ti * (ti + 1) / 2 > t) --ti;
@@ -127,13 +148,24 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   tile_update(A, A, A, n, ci, cj, ci, cj, k0, min(LB, n - k0));
 }
 
+__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int n, int k0,
+                                                          const int* __restrict__ info) {
+  chol_update_body(A, n, k0, info, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void chol_update_batch_kernel(PrepBatch b, int k0) {
+  const int i = blockIdx.y;
+  const int T = (b.n[i] - k0 - LB + LB - 1) / LB;  // trailing tiles per side of output i
+  if (T > 0 && (int)blockIdx.x < T * (T + 1) / 2) chol_update_body(b.A[i], b.n[i], k0, b.info[i], blockIdx.x);
+}
+
 // ---------------------------------------------------------------------------
 // Triangular inverse X = L^{-1} (lower), right-looking by block rows of the
 // right-hand side I: at step k0 the block row X_k = Lkk^{-1} B_k (B_k holds
 // I_k minus the updates so far, columns < k0 + nb), then
 // B_i -= L_ik X_k for every later block row i.  X overwrites B in `X`.
-__global__ __launch_bounds__(256) void trinv_panel_kernel(const double* __restrict__ L, double* __restrict__ X, int n,
-                                                          int k0, const int* __restrict__ info) {
+__device__ __forceinline__ void trinv_panel_body(const double* __restrict__ L, double* __restrict__ X, int n, int k0,
+                                                 const int* __restrict__ info) {
   __shared__ double Lk[LB][LB + 1];
   if (*info != 0) return;
   const int nb = min(LB, n - k0);
@@ -156,6 +188,7 @@ __global__ __launch_bounds__(256) void trinv_panel_kernel(const double* __restri
         for (int q = 0; q < r; ++q) s -= Lk[r][q] * x[q];
         x[r] = s / Lk[r][r];
       }
+      asm volatile("" ::: "memory");  // as in chol_panel_kernel: one row of Lk live at a time
     }
 #pragma unroll
     for (int r = 0; r < LB; ++r)
@@ -163,17 +196,27 @@ __global__ __launch_bounds__(256) void trinv_panel_kernel(const double* __restri
   }
 }
 
+__global__ __launch_bounds__(256) void trinv_panel_kernel(const double* __restrict__ L, double* __restrict__ X, int n,
+                                                          int k0, const int* __restrict__ info) {
+  trinv_panel_body(L, X, n, k0, info);
+}
+
+__global__ __launch_bounds__(256) void trinv_panel_batch_kernel(PrepBatch b, int k0) {
+  const int i = blockIdx.y;
+  if (k0 < b.n[i]) trinv_panel_body(b.A[i], b.X[i], b.n[i], k0, b.info[i]);
+}
+
 // B_i[:, 0 : k0 + nb) -= L[i-block, k-block] X_k for block rows i > k; grid
 // (column tiles of the first k0 + nb columns, later block rows).
-__global__ __launch_bounds__(256) void trinv_update_kernel(const double* __restrict__ L, double* __restrict__ X, int n,
-                                                           int k0, const int* __restrict__ info) {
+__device__ __forceinline__ void trinv_update_body(const double* __restrict__ L, double* __restrict__ X, int n, int k0,
+                                                  const int* __restrict__ info, int bx, int by) {
   if (*info != 0) return;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int si = wave >> 1, sj = wave & 1;
   const int nb = min(LB, n - k0);
-  const int ci = k0 + LB * (1 + blockIdx.y);  // output rows
-  const int cj = LB * blockIdx.x;             // output columns
+  const int ci = k0 + LB * (1 + by);  // output rows
+  const int cj = LB * bx;             // output columns
   const int ra = ci + 16 * si + (lane & 15);  // row of L (A operand)
   const int cb = cj + 16 * sj + (lane & 15);  // column of X_k (B operand)
   d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -190,6 +233,19 @@ __global__ __launch_bounds__(256) void trinv_update_kernel(const double* __restr
     const int col = cj + 16 * sj + (lane & 15);
     if (row < n && col < k0 + nb) X[(size_t)row * n + col] -= acc[r];
   }
+}
+
+__global__ __launch_bounds__(256) void trinv_update_kernel(const double* __restrict__ L, double* __restrict__ X, int n,
+                                                           int k0, const int* __restrict__ info) {
+  trinv_update_body(L, X, n, k0, info, blockIdx.x, blockIdx.y);
+}
+
+__global__ __launch_bounds__(256) void trinv_update_batch_kernel(PrepBatch b, int k0) {
+  const int i = blockIdx.z;
+  const int n = b.n[i];
+  if (k0 >= n) return;
+  const int rows = (n - k0 - LB + LB - 1) / LB, cols = (k0 + LB + LB - 1) / LB;
+  if ((int)blockIdx.x < cols && (int)blockIdx.y < rows) trinv_update_body(b.A[i], b.X[i], n, k0, b.info[i], blockIdx.x, blockIdx.y);
 }
 
 // X = I (row-major n x n) and the upper triangle of L zeroed.
@@ -212,16 +268,24 @@ __global__ __launch_bounds__(1024) void alpha_kernel(const double* __restrict__ 
   if (*info != 0) return;
   for (int i = threadIdx.x; i < n; i += blockDim.x) r[i] = y[i] - c;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  // t = X r, one row per wave (lanes along the row: coalesced reads), lane partial sums in q order
+  // then a fixed-order wave reduction
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int i = wave; i < n; i += nw) {
     double s = 0.0;
-    for (int q = 0; q <= i; ++q) s = fma(X[(size_t)i * n + q], r[q], s);
-    t[i] = s;
+    for (int q = lane; q <= i; q += 64) s = fma(X[(size_t)i * n + q], r[q], s);
+    s = wave_sum(s);
+    if (lane == 0) t[i] = s;
   }
   __syncthreads();
+  // alpha = X^T t, one column q per thread summed over i in ascending order; unrolled so that eight
+  // rows' loads are in flight at once (they do not depend on the running sum)
   for (int q = threadIdx.x; q < pad16(n); q += blockDim.x) {
     double s = 0.0;
-    if (q < n)
+    if (q < n) {
+#pragma unroll 8
       for (int i = q; i < n; ++i) s = fma(X[(size_t)i * n + q], t[i], s);  // coalesced across q
+    }
     alpha[q] = s;
   }
 }
@@ -261,6 +325,33 @@ hipError_t launch_tri_inverse(double* L, double* X, int n, const int* info, hipS
     const int rows = (n - k0 - LB + LB - 1) / LB;
     const int cols = (k0 + LB + LB - 1) / LB;
     if (rows > 0) hipLaunchKernelGGL(trinv_update_kernel, dim3(cols, rows), dim3(256), 0, s, L, X, n, k0, info);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cholesky_batch(const PrepBatch& b, int m, hipStream_t s) {
+  int nmax = 0;
+  for (int i = 0; i < m; ++i) nmax = std::max(nmax, b.n[i]);
+  for (int k0 = 0; k0 < nmax; k0 += LB) {
+    hipLaunchKernelGGL(chol_panel_batch_kernel, dim3(1, m), dim3(256), 0, s, b, k0);
+    const int T = (nmax - k0 - LB + LB - 1) / LB;
+    if (T > 0) hipLaunchKernelGGL(chol_update_batch_kernel, dim3(T * (T + 1) / 2, m), dim3(256), 0, s, b, k0);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_tri_inverse_batch(const PrepBatch& b, int m, hipStream_t s) {
+  int nmax = 0;
+  for (int i = 0; i < m; ++i) {
+    nmax = std::max(nmax, b.n[i]);
+    hipLaunchKernelGGL(trinv_init_kernel, dim3(grid_for((size_t)b.n[i] * b.n[i])), dim3(256), 0, s, b.A[i], b.X[i],
+                       b.n[i]);
+  }
+  for (int k0 = 0; k0 < nmax; k0 += LB) {
+    hipLaunchKernelGGL(trinv_panel_batch_kernel, dim3(1, m), dim3(256), 0, s, b, k0);
+    const int rows = (nmax - k0 - LB + LB - 1) / LB;
+    const int cols = (k0 + LB + LB - 1) / LB;
+    if (rows > 0) hipLaunchKernelGGL(trinv_update_batch_kernel, dim3(cols, rows, m), dim3(256), 0, s, b, k0);
   }
   return hipGetLastError();
 }

@@ -61,6 +61,9 @@ SIGNATURES = {
     "dkg_prepare_workspace": (c_size_t, [c_int]),
     "dkg_prepare_output": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_void_p, c_size_t,
                                    c_void_p, c_void_p, POINTER(c_double), c_void_p]),
+    "dkg_prepare_outputs": (c_int, [POINTER(DkgOutput), c_int, c_int, POINTER(c_void_p), c_int, POINTER(c_void_p),
+                                    POINTER(c_void_p), POINTER(c_size_t), POINTER(c_void_p), POINTER(c_void_p),
+                                    POINTER(c_double), c_void_p]),
     "dkg_cross_root": (c_int, [POINTER(DkgOutput), c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "dkg_forward_workspace": (c_size_t, [POINTER(DkgOutput), c_int, c_int, c_int, c_int]),
     "dkg_forward": (c_int, [POINTER(DkgOutput), c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,

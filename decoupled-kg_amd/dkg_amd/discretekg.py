@@ -97,6 +97,30 @@ def _fingerprint(obj):
     return id(obj)
 
 
+# Device states of recently used (model, discretisation) pairs.  The reference builds one acquisition
+# per output on the same fitted model and grid (acquisition_optimisation_strategy.py:209-216, one
+# DiscreteKnowledgeGradient per obj_idx_new), and every one reads the same posterior caches: they share
+# one DeviceGPState instead of each repeating the Cholesky, the inverse and the cross products.  An entry
+# holds its model's tensors alive, so no live tensor can take over an id in its fingerprint.
+_STATE_CACHE: list = []
+_STATE_CACHE_SIZE = 4
+
+
+def shared_state(state: ModelListGPState, fp, x_discretisation: Tensor, device, owner=None) -> DeviceGPState:
+    """The cached DeviceGPState of (model fingerprint ``fp``, discretisation values, device), or a new one.
+    ``owner`` (the caller's model object) is kept alive with the entry, with its fingerprinted tensors."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    D = x_discretisation.detach()
+    for i, (efp, eD, edev, est, _) in enumerate(_STATE_CACHE):
+        if efp == fp and edev == dev and eD.shape == D.shape and eD.dtype == D.dtype and torch.equal(eD, D.to(eD.device)):
+            _STATE_CACHE.insert(0, _STATE_CACHE.pop(i))
+            return est
+    st = DeviceGPState(state, x_discretisation, dev)
+    _STATE_CACHE.insert(0, (fp, D.clone(), dev, st, owner))
+    del _STATE_CACHE[_STATE_CACHE_SIZE:]
+    return st
+
+
 class _ForwardFn(torch.autograd.Function):
     """Device forward; when X requires grad the same C call also returns
     dKG(x_b)/dx_b (dkg_plan_forward_grad), and backward scales it by the
@@ -199,7 +223,7 @@ class DiscreteKnowledgeGradient(_Base):
                 self._target_error = IndexError("list index out of range")
         self._device = device
         self._fp = _fingerprint(model)
-        self._state = DeviceGPState(state, x_discretisation, device)
+        self._state = shared_state(state, self._fp, x_discretisation, device, owner=model)
         self._W = scalarisation_weights.detach().to(self._state.device, torch.double).contiguous()
         self._plan = None
         self._plan_grad = None
@@ -208,7 +232,8 @@ class DiscreteKnowledgeGradient(_Base):
         """Rebuild the device state if the model changed since it was read (see _fingerprint)."""
         fp = _fingerprint(self.model)
         if fp != self._fp:
-            self._state = DeviceGPState(_as_model_state(self.model), self.x_discretisation, self._device)
+            self._state = shared_state(_as_model_state(self.model), fp, self.x_discretisation, self._device,
+                                       owner=self.model)
             self._plan = None
             self._plan_grad = None
             self._fp = fp

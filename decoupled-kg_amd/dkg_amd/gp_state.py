@@ -74,40 +74,54 @@ def _base_struct(st: SingleTaskGPState, inv_ls, train_x) -> _lib.DkgOutput:
     return o
 
 
-def prepare_output(st: SingleTaskGPState, D: torch.Tensor) -> OutputCache:
-    """Build one output's device caches over the discretisation ``D`` (device, N x d)."""
+def prepare_outputs(models, D: torch.Tensor) -> List[OutputCache]:
+    """Every output's device caches over the discretisation ``D`` (device, N x d): the factorisations of
+    all outputs side by side (dkg_prepare_outputs: one chain of launches, one status check), then each
+    output's Q_D and mu_D (dkg_cross_root)."""
     lib = _lib.load()
     dev = D.device
     stream = current_stream_ptr(dev)
-    n, d = st.train_x.shape
     N = D.shape[0]
-    if _pad16(n) > 1024:
-        raise UnsupportedError(f"n={n} training points > 1024 per output is not supported")
-    X = st.train_x.to(dev).contiguous()
-    inv_ls = (1.0 / st.lengthscale).to(dev).contiguous()
-    o = _base_struct(st, inv_ls, X)
+    parts = []
+    for st in models:
+        n, d = st.train_x.shape
+        if _pad16(n) > 1024:
+            raise UnsupportedError(f"n={n} training points > 1024 per output is not supported")
+        X = st.train_x.to(dev).contiguous()
+        inv_ls = (1.0 / st.lengthscale).to(dev).contiguous()
+        o = _base_struct(st, inv_ls, X)
+        y = st.train_y.to(dev).contiguous()
+        L = torch.empty(n, n, dtype=torch.double, device=dev)
+        work = torch.empty(lib.dkg_prepare_workspace(n), dtype=torch.uint8, device=dev)
+        alpha = torch.empty(_pad16(n), dtype=torch.double, device=dev)
+        root_frag = torch.empty(lib.dkg_frag_elems(n, n), dtype=torch.double, device=dev)
+        parts.append((st, o, X, inv_ls, y, L, work, alpha, root_frag))
+    m = len(parts)
+    d = D.shape[1]
+    outs = (_lib.DkgOutput * m)(*[p[1] for p in parts])
+    ptrs = lambda k: (ctypes.c_void_p * m)(*[_lib.ptr(p[k]) for p in parts])  # noqa: E731
+    jit = (ctypes.c_double * m)()
+    wbytes = (ctypes.c_size_t * m)(*[p[6].numel() for p in parts])
+    _lib.check(lib.dkg_prepare_outputs(outs, m, d, ptrs(4), 3, ptrs(5), ptrs(6), wbytes, ptrs(7), ptrs(8), jit, stream),
+               "dkg_prepare_outputs")
+    caches = []
+    for i, (st, o, X, inv_ls, y, L, work, alpha, root_frag) in enumerate(parts):
+        o.alpha = _lib.ptr(alpha)
+        o.root_frag = _lib.ptr(root_frag)
+        disc_frag = torch.empty(max(1, lib.dkg_frag_elems(N, o.n)), dtype=torch.double, device=dev)
+        disc_mean = torch.empty(max(16, _pad16(N)), dtype=torch.double, device=dev)
+        if N > 0:
+            _lib.check(lib.dkg_cross_root(o, d, _lib.ptr(D), N, _lib.ptr(disc_frag), _lib.ptr(disc_mean), stream),
+                       "dkg_cross_root")
+        o.disc_frag = _lib.ptr(disc_frag)
+        o.disc_mean = _lib.ptr(disc_mean)
+        caches.append(OutputCache(st, inv_ls, X, alpha, root_frag, disc_frag, disc_mean, L, jit[i], o))
+    return caches
 
-    y = st.train_y.to(dev).contiguous()
-    L = torch.empty(n, n, dtype=torch.double, device=dev)
-    work = torch.empty(lib.dkg_prepare_workspace(n), dtype=torch.uint8, device=dev)
-    alpha = torch.empty(_pad16(n), dtype=torch.double, device=dev)
-    root_frag = torch.empty(lib.dkg_frag_elems(n, n), dtype=torch.double, device=dev)
-    jitter = ctypes.c_double(0.0)
-    _lib.check(lib.dkg_prepare_output(o, d, _lib.ptr(y), 3, _lib.ptr(L), _lib.ptr(work), work.numel(),
-                                      _lib.ptr(alpha), _lib.ptr(root_frag), ctypes.byref(jitter), stream),
-               "dkg_prepare_output")
-    del work
-    o.alpha = _lib.ptr(alpha)
-    o.root_frag = _lib.ptr(root_frag)
 
-    disc_frag = torch.empty(max(1, lib.dkg_frag_elems(N, n)), dtype=torch.double, device=dev)
-    disc_mean = torch.empty(max(16, _pad16(N)), dtype=torch.double, device=dev)
-    if N > 0:
-        _lib.check(lib.dkg_cross_root(o, d, _lib.ptr(D), N, _lib.ptr(disc_frag), _lib.ptr(disc_mean), stream),
-                   "dkg_cross_root")
-    o.disc_frag = _lib.ptr(disc_frag)
-    o.disc_mean = _lib.ptr(disc_mean)
-    return OutputCache(st, inv_ls, X, alpha, root_frag, disc_frag, disc_mean, L, jitter.value, o)
+def prepare_output(st: SingleTaskGPState, D: torch.Tensor) -> OutputCache:
+    """One output's device caches (prepare_outputs of one)."""
+    return prepare_outputs([st], D)[0]
 
 
 class DeviceGPState:
@@ -126,7 +140,7 @@ class DeviceGPState:
         self.model = model
         self.D = x_discretisation.detach().to(self.device, torch.double).contiguous()
         self.N, self.d = self.D.shape
-        self.outputs: List[OutputCache] = [prepare_output(m, self.D) for m in model.models]
+        self.outputs: List[OutputCache] = prepare_outputs(model.models, self.D)
         self.m = len(self.outputs)
         self.structs = (_lib.DkgOutput * self.m)(*[c.struct for c in self.outputs])
         self._ws = None

@@ -111,6 +111,14 @@ size_t dkg_prepare_workspace(int n);
 int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int max_tries, double* L, void* work,
                        size_t work_bytes, double* alpha, double* root_frag, double* jitter_used, void* stream);
 
+/* dkg_prepare_output for m outputs at once (host arrays of m per-output pointers): every launch of
+ * the first Cholesky attempt and of the inverse carries all outputs (one workgroup column per output),
+ * one synchronisation checks all the factorisations, and only outputs that failed are retried with
+ * jitter, one by one.  Same results as m calls of dkg_prepare_output.  jitter_used: host [m]. */
+int dkg_prepare_outputs(const dkg_output* outs, int m, int d, const double* const* train_y, int max_tries,
+                        double* const* L, void* const* work, const size_t* work_bytes, double* const* alpha,
+                        double* const* root_frag, double* jitter_used, void* stream);
+
 /* Pack dense row-major R (n x n, device) into o->root_frag layout (device). */
 int dkg_pack_root(const double* r, int n, double* root_frag, void* stream);
 

@@ -197,3 +197,25 @@ def test_candidates_in_kernel_arguments_match_the_copy_path(B):
         Xs = torch.stack([Xb, Xb], -1)[..., 0]
         kg2, g2 = plan.forward_grad_host(Xs)
         assert torch.equal(kg2, kg) and torch.equal(g2, g)
+
+
+def test_acquisitions_on_one_model_share_the_device_state():
+    """One DeviceGPState per (model, discretisation): the per-output acquisitions the reference builds on
+    one fitted model (acquisition_optimisation_strategy.py:209-216) share it; a changed model or grid
+    gets its own, and the values are those of a fresh state."""
+    from dkg_amd.gp_state import DeviceGPState
+
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    a0 = DiscreteKnowledgeGradient(model, D, W, target_output_ix=0)
+    a1 = DiscreteKnowledgeGradient(model, D.clone(), W, target_output_ix=1)
+    af = DiscreteKnowledgeGradient(model, D, W)
+    assert a0._state is a1._state is af._state
+    Xb = X[:8].unsqueeze(-2)
+    fresh = DeviceGPState(model, D)
+    for acq, t in ((a0, 0), (a1, 1), (af, None)):
+        assert torch.equal(acq(Xb).cpu(), fresh.forward(X[:8].to(DEV), W, t).cpu())
+    other = DiscreteKnowledgeGradient(model, D + 0.01, W)
+    assert other._state is not a0._state
+    model.models[0].train_y.add_(1.0)  # an in-place edit: the next forward rebuilds, the old entry stays put
+    a0(Xb)
+    assert a0._state is not a1._state

@@ -18,4 +18,5 @@ for f in sys.argv[1:]:
               "roof": (r["kernel"], round(r["frac"], 4), r.get("valu_busy_frac")),
               "b1": round(b1.get("median_us", 0), 1), "b1 autograd": round((b1.get("autograd_route") or {}).get("median_us", 0), 1),
               "exposed_ms": (d.get("per_rank") or {}).get("exposed_collective_ms"),
+              "prep_ms": round((d.get("state_prep") or {}).get("ms_median", 0), 3),
               "cpu": (d.get("cpu_baseline") or {}).get("value")})
