@@ -45,6 +45,7 @@ struct WsLayout {
   size_t var[DKG_MAX_OUTPUTS];
   size_t mux_all, var_all, cov_all, mu_all;
   size_t wg_part;
+  size_t wg_gpart;
   size_t tickets;
   size_t hull_pairs;
   size_t total;
@@ -101,6 +102,8 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
   envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split);
   L.wg_part = off;
   off = align256(off + (size_t)std::max(B, 1) * split * sizeof(double));
+  L.wg_gpart = off;  // value+gradient with split > 2: the gradient's per-workgroup partials, summed in order
+  off = align256(off + ((flags & DKG_PLAN_GRAD) && split > 2 ? (size_t)std::max(B, 1) * split * d * sizeof(double) : 0));
   L.tickets = off;
   off = align256(off + Bp * sizeof(int));
   L.hull_pairs = off;
@@ -201,6 +204,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->cov_stride = (int64_t)std::max(N, 1) * cov_rec(m);
   P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
+  P->wg_gpart = reinterpret_cast<double*>(ws + L.wg_gpart);
   P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
   static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
   static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
@@ -556,7 +560,7 @@ int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const dou
 }
 
 int dkg_plan_forward_grad_hostx(const void* host_plan, const void* dev_plan, const double* x_host, double* x_dev,
-                                int B, double* kg, double* dkg_dx, void* stream) {
+                                int B, double* kg, double* dkg_dx, double* out_host, void* stream) {
   if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
   const Plan& h = *static_cast<const Plan*>(host_plan);
   if (!h.grad) return fail(DKG_ERR_ARG, "plan was not initialised with DKG_PLAN_GRAD");
@@ -569,8 +573,11 @@ int dkg_plan_forward_grad_hostx(const void* host_plan, const void* dev_plan, con
   XArg xa;
   xa.n = B * h.d;
   for (int i = 0; i < xa.n; ++i) xa.v[i] = x_host[i];
-  return hip_check(launch_forward_grad(h, static_cast<const Plan*>(dev_plan), x_dev, B, kg, dkg_dx,
-                                       (hipStream_t)stream, &xa), "forward_grad_hostx");
+  int st = hip_check(launch_forward_grad(h, static_cast<const Plan*>(dev_plan), x_dev, B, kg, dkg_dx,
+                                         (hipStream_t)stream, &xa, out_host),
+                     "forward_grad_hostx");
+  if (st || !out_host) return st;
+  return hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");  // out_host is filled
 }
 
 int dkg_plan_status(const void* host_plan, int* err, int reset, void* stream) {

@@ -1176,7 +1176,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
                                               const double* __restrict__ var_all,
                                               const double* __restrict__ mux_all, const double* __restrict__ wts,
                                               long long cov_stride, int bpad, int b, int g, int G, double* smem,
-                                              unsigned long long* st, const Handoff* ho = nullptr) {
+                                              unsigned long long* st, const Handoff* ho = nullptr,
+                                              double* __restrict__ hout = nullptr) {
   static_assert(!HO || (!GRAD && !STREAM), "the fused forward stages its lines (no gradient, no streaming)");
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space)
   __shared__ double s_pp[DKG_MAX_OUTPUTS * 6];
@@ -1966,13 +1967,21 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
 #ifndef DKG_STG_STAMPS
   if (!GRAD) KST(st, 5);
 #endif
+  __shared__ int s_lastk;  // G > 2: this workgroup arrived last for its candidate (kg's ticket)
   if constexpr (GRAD) {
     if (threadIdx.x < d) {
       double gs = 0.0;
       for (int w2 = 0; w2 < SW; ++w2) gs += sgw[w2 * 64 + 48 + threadIdx.x];
-      // at most two workgroups per candidate (S <= 16): commutative, deterministic
-      atomicAdd(&dkg[(size_t)b * d + threadIdx.x], gs / (double)S);
+      if (G <= 2) {
+        // at most two workgroups per candidate (S <= 16): two addends onto a zeroed cell commute
+        atomicAdd(&dkg[(size_t)b * d + threadIdx.x], gs / (double)S);
+      } else {
+        // more: per-workgroup partials, summed in workgroup order by the last to arrive (below)
+        P->wg_gpart[((size_t)b * G + g) * d + threadIdx.x] = gs / (double)S;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      }
     }
+    if (G > 2) __syncthreads();  // the partials are out before thread 0 takes the ticket
   }
   if (threadIdx.x == 0) {
     double s = 0.0;
@@ -1988,6 +1997,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int prev = atomicAdd(&P->tickets[b], 1);
+      s_lastk = prev == G - 1;
       if (prev == G - 1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1995,6 +2005,54 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
         for (int q = 0; q < G; ++q)
           tot += __hip_atomic_load(&P->wg_part[(size_t)b * G + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         kg[b] = tot / (double)S;
+        if constexpr (GRAD) {
+          if (hout != nullptr) hout[b] = kg[b];
+        }
+      }
+    }
+  }
+  if constexpr (GRAD) {
+    if (G > 2) {
+      __syncthreads();
+      if (s_lastk && threadIdx.x < d) {  // the last workgroup: the gradient's partials in workgroup order
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        double tot = 0.0;
+        for (int q = 0; q < G; ++q)
+          tot += __hip_atomic_load(&P->wg_gpart[((size_t)b * G + q) * d + threadIdx.x], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        dkg[(size_t)b * d + threadIdx.x] = tot;
+        if (hout != nullptr) hout[(size_t)B + (size_t)b * d + threadIdx.x] = tot;
+      }
+    }
+  }
+  if constexpr (GRAD) {
+    // hout (dkg_plan_forward_grad_hostx): the candidate's KG and dKG/dx straight into the caller's pinned
+    // host buffer [kg (B) | dkg (B x d)], so no copy follows the launch.  One or two workgroups per
+    // candidate: the second to arrive (ticket; the cross stage zeroed it) reads the sums back after an
+    // acquire.  More: the last workgroup writes them with the ordered sums above.
+    if (hout != nullptr && G <= 2) {
+      __shared__ int s_last;
+      __syncthreads();  // every thread's atomics are issued
+      if (threadIdx.x == 0) {
+        int last = 1;
+        if (G == 2) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          last = atomicAdd(&P->tickets[b], 1) == 1;
+          if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+        s_last = last;
+      }
+      __syncthreads();
+      if (s_last) {
+        if (threadIdx.x == 0)
+          hout[b] = __hip_atomic_load(&kg[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x < d)
+          hout[(size_t)B + (size_t)b * d + threadIdx.x] =
+              __hip_atomic_load(&dkg[(size_t)b * d + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -2028,11 +2086,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ var_all,
                                                        const double* __restrict__ mux_all,
                                                        const double* __restrict__ wts, long long cov_stride,
-                                                       int bpad) {
+                                                       int bpad, double* __restrict__ hout) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
   envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
-                                       cov_stride, bpad, blockIdx.x, blockIdx.y, gridDim.y, smem, kst_slot(dst, P, 2));
+                                       cov_stride, bpad, blockIdx.x, blockIdx.y, gridDim.y, smem, kst_slot(dst, P, 2),
+                                       nullptr, hout);
 }
 
 // The lines of every (candidate, scalarisation) pair of the plan's last
@@ -2100,6 +2159,7 @@ struct EnvLaunch {
   int dst;
   const double* xnew;  // GRAD
   double* dkg;         // GRAD
+  double* hout;        // GRAD: pinned host [kg | dkg] (dkg_plan_forward_grad_hostx), nullable
 };
 
 template <int MAXL, int M, bool GRAD, bool STREAM>
@@ -2108,7 +2168,7 @@ hipError_t launch_env_t(const EnvLaunch& a) {
   const Plan& h = *a.host;
   hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights,
-                     (long long)h.cov_stride, h.bpad);
+                     (long long)h.cov_stride, h.bpad, a.hout);
   return hipGetLastError();
 }
 

@@ -50,7 +50,8 @@ struct Plan {
   double* mu_all;                   // [N][cov_rec(m)] the outputs' disc_mean, line records
   int64_t cov_stride;               // N * cov_rec(m): doubles per candidate in cov_all
   double* wg_part;                  // [B x split] partial sums (split > 2 only)
-  int* tickets;                     // [B] arrival counters (split > 2 only)
+  int* tickets;                     // [B] arrival counters (split > 2; value+gradient with a host output: split 2)
+  double* wg_gpart;                 // GRAD: [B x split x d] per-workgroup dKG/dx partials (split > 2 only)
   float* q32[DKG_MAX_OUTPUTS];      // F32: quad-packed K(x, X) R per output (workspace)
   float* root32[DKG_MAX_OUTPUTS];   // F32: quad-packed R^T (fp32 copy of root_frag, plan init)
   float* disc32[DKG_MAX_OUTPUTS];   // F32: quad-packed Q_D (fp32 copy of disc_frag, plan init)
@@ -101,8 +102,9 @@ struct XArg {
   double v[DKG_XARG_MAX];
   int n;
 };
+// hout (nullable): pinned host [kg (B) | dkg (B x d)] written by the envelope stage itself (split <= 2).
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
-                               hipStream_t s, const XArg* xa = nullptr);
+                               hipStream_t s, const XArg* xa = nullptr, double* hout = nullptr);
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream);
 // One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,

@@ -412,7 +412,7 @@ static hipError_t launch_cross_fwd_grad_t(const Plan& h, const Plan* dev, const 
 }
 
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
-                               hipStream_t s, const XArg* xa) {
+                               hipStream_t s, const XArg* xa, double* hout) {
   hipError_t e;
   XArg none;
   none.n = 0;
@@ -426,7 +426,8 @@ hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xne
   if (e != hipSuccess) return e;
   if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 1)) != hipSuccess) return e;  // cov rows, variances
   EnvLaunch a{&h, dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
-              envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, h.debug_stamp, xnew, dkg};
+              envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, h.debug_stamp, xnew, dkg,
+              hout};
   return launch_env<true>(h, a);
 }
 

@@ -142,23 +142,32 @@ class _ForwardFn(torch.autograd.Function):
 
 
 class _HostForwardFn(torch.autograd.Function):
-    """``forward`` of host candidates (what ``optimize_acqf`` passes: a host X with ``requires_grad``):
-    one device round trip per call -- a pinned H2D copy of X, the forward's launches (with dKG/dx when
-    X requires grad) and one pinned D2H copy of the results -- and a host-side backward.  The same
-    kernels as ``_ForwardFn``, so the same bits."""
+    """``forward`` of host candidates (what ``optimize_acqf`` passes: a host X [*batch, 1, d] with
+    ``requires_grad``): one device round trip per call -- with a gradient, the candidates in the first
+    kernel's arguments and [KG | dKG/dx] written by the envelope kernel into pinned memory
+    (``ForwardPlan.forward_grad_host``); without, a pinned copy each way -- and a host-side backward.
+    The reshapes and the dtype round trip happen inside, so the autograd graph is this one node.  The
+    same kernels as ``_ForwardFn``, so the same bits."""
 
     @staticmethod
     def forward(ctx, X, acq):
+        d = X.shape[-1]
+        batch = X.shape[:-2]
+        flat = X.detach().reshape(-1, d)
+        if flat.dtype != torch.double:
+            flat = flat.to(torch.double)
         if ctx.needs_input_grad[0]:
-            kg, dkg = acq._plan_for(X.shape[0], grad=True).forward_grad_host(X)
+            kg, dkg = acq._plan_for(flat.shape[0], grad=True).forward_grad_host(flat)
             ctx.save_for_backward(dkg)
-            return kg
-        return acq._plan_for(X.shape[0]).forward_host(X)
+            ctx.xshape, ctx.xdtype = X.shape, X.dtype
+        else:
+            kg = acq._plan_for(flat.shape[0]).forward_host(flat.contiguous())
+        return kg.to(X.dtype).reshape(batch)
 
     @staticmethod
     def backward(ctx, grad):
         (dkg,) = ctx.saved_tensors
-        return grad.to(dkg)[:, None] * dkg, None
+        return (grad.reshape(-1, 1).to(dkg) * dkg).reshape(ctx.xshape).to(ctx.xdtype), None
 
 
 class DiscreteKnowledgeGradient(_Base):
@@ -267,10 +276,9 @@ class DiscreteKnowledgeGradient(_Base):
                 f"Expected X to have last dimension matching 'self.x_discretisation'. "
                 f"Got {X.shape[-1]=}, {self.x_discretisation.shape[-1]=}.")
         self._refresh()
-        flat = X.reshape(-1, d)
         if X.device.type == "cpu":  # the host route: one round trip (and a host backward)
-            kg = _HostForwardFn.apply(flat.to(torch.double).contiguous(), self)
-            return kg.to(dtype=X.dtype).reshape(batch_shape)
+            return _HostForwardFn.apply(X, self)
+        flat = X.reshape(-1, d)
         Xd = flat.to(self._state.device, torch.double)
         kg = _ForwardFn.apply(Xd, self)
         return kg.to(device=X.device, dtype=X.dtype).reshape(batch_shape)

@@ -195,6 +195,7 @@ class ForwardPlan:
         self.fused = bool(lib.dkg_plan_fused(self.host))  # forward_into is one fused launch
         self._fwd = lib.dkg_plan_forward
         self._fwd_timed = lib.dkg_plan_forward_timed
+        self._fwd_grad_hostx = lib.dkg_plan_forward_grad_hostx
         self._dev_ptr = _lib.ptr(self.dev)
 
     def status(self, reset: bool = False) -> int:
@@ -260,13 +261,14 @@ class ForwardPlan:
         """KG[B] and dKG/dx [B, d] for host candidates X (B x d), returned as host tensors: the L-BFGS-B
         evaluation of ``optimize_acqf`` (``bo_loop.py:127-129``), whose host needs both back every call.
 
-        One pinned H2D copy of X into a plan-owned device buffer, the launches of ``dkg_plan_forward_grad``
-        (eager, the default) writing KG and dKG/dx side by side into one device buffer, one pinned D2H copy
-        of that buffer and one event wait: a single device round trip instead of one per output.  Everything
-        is ordered on the current stream of the plan's device (which need not be the current device), and
-        the completion event is recorded there.  With ``graph`` the launches are a HIP graph captured once
-        per batch size (fixed pointers, so replay is one host call; measured slower than eager launches at
-        B = 1); the results are the same bits as ``forward_grad``."""
+        B x d <= DKG_XARG_MAX (the default path): one C call (``dkg_plan_forward_grad_hostx``) -- the
+        candidates travel in the first kernel's arguments, the envelope kernel writes [KG | dKG/dx] into a
+        plan-owned pinned buffer, the call returns after the stream has finished -- then one host copy
+        out.  Larger batches, or ``graph``: one pinned H2D copy of X, the launches of
+        ``dkg_plan_forward_grad`` (eager, or a HIP graph captured once per batch size; measured slower than
+        eager launches at B = 1), one pinned D2H copy and one event wait.  Everything is
+        ordered on the current stream of the plan's device; the results are the same bits as
+        ``forward_grad``."""
         if not self.grad:
             raise ValueError("plan was built without grad=True")
         B, d = X_host.shape[0], self.state.d
@@ -276,8 +278,32 @@ class ForwardPlan:
             raise ValueError(f"{B} candidates > plan capacity {self.max_B}")
         if B == 0:
             return torch.empty(0, dtype=torch.double), torch.empty(0, d, dtype=torch.double)
+        if not graph and B * d <= _lib.DKG_XARG_MAX and torch.cuda.current_device() == self.device.index:
+            return self._forward_grad_hostx(X_host, B, d)
         with torch.cuda.device(self.device):
+            if not graph and B * d <= _lib.DKG_XARG_MAX:
+                return self._forward_grad_hostx(X_host, B, d)
             return self._forward_grad_host(X_host, B, d, graph)
+
+    def _forward_grad_hostx(self, X_host: torch.Tensor, B: int, d: int):
+        # the plan's device is current; one C call launches, lets the envelope kernel write the pinned
+        # buffer and synchronises the stream
+        io = self._io.get(B) if getattr(self, "_io", None) is not None else None
+        if io is None:
+            self._host_buffers(d)
+            dx = self._dx[:B * d]
+            io = self._io[B] = (dx.data_ptr(), self._dout[:B].data_ptr(), self._dout[B:B * (d + 1)].data_ptr(),
+                                self._hout[:B * (d + 1)])
+        xc = X_host
+        if xc.dtype != torch.double or not xc.is_contiguous():
+            xc = xc.to(torch.double).contiguous()
+        out = io[3]
+        st = self._fwd_grad_hostx(self.host, self._dev_ptr, xc.data_ptr(), io[0], B, io[1], io[2], out.data_ptr(),
+                                  _raw_stream(self.device))
+        if st:
+            _lib.check(st, "dkg_plan_forward_grad_hostx")
+        r = out.clone()
+        return r[:B], r[B:].view(B, d)
 
     def _host_buffers(self, d: int):
         """The pinned host and device staging buffers of the host entries (made once, sized for max_B)."""
@@ -302,24 +328,6 @@ class ForwardPlan:
             _lib.check(lib.dkg_plan_forward_grad(self.host, self._dev_ptr, _lib.ptr(dx), B, _lib.ptr(kg),
                                                  _lib.ptr(dkg), stream), "dkg_plan_forward_grad")
 
-        if not graph and B * d <= _lib.DKG_XARG_MAX:
-            # the candidates ride in the first kernel's arguments: no host-to-device copy (~20 us at B = 1)
-            xc = X_host.detach().reshape(B, d)
-            if xc.dtype != torch.double or not xc.is_contiguous():
-                xc = xc.to(torch.double).contiguous()
-            io = self._io.get(B)
-            if io is None:  # per batch size: the raw pointers and the pinned result views
-                io = self._io[B] = (_lib.ptr(dx), _lib.ptr(kg), _lib.ptr(dkg), self._hout[:B * (d + 1)],
-                                    self._dout[:B * (d + 1)])
-            st = lib.dkg_plan_forward_grad_hostx(self.host, self._dev_ptr, xc.data_ptr(), io[0], B, io[1], io[2],
-                                                 _raw_stream(self.device))
-            if st:
-                _lib.check(st, "dkg_plan_forward_grad_hostx")
-            out = io[3]
-            out.copy_(io[4], non_blocking=True)
-            self._done.record()
-            self._done.synchronize()
-            return out[:B].clone(), out[B:].view(B, d).clone()
         hx = self._hx[:B * d].view(B, d)
         hx.copy_(X_host.detach().reshape(B, d))
         dx.copy_(hx, non_blocking=True)

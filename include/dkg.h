@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 5
+#define DKG_ABI_VERSION 6
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -216,9 +216,12 @@ int dkg_plan_forward_grad(const void* host_plan, const void* dev_plan, const dou
  * the candidates travel inside the first kernel's arguments instead of a host-to-device copy
  * (one copy fewer on the optimize_acqf L-BFGS-B path, batch_limit = 1: bo_loop.py:127-129), and
  * that kernel leaves them in x_dev (device, B x d) for the later kernels.  x_host may be reused as
- * soon as this returns.  Same results, bit for bit, as dkg_plan_forward_grad on x_dev. */
+ * soon as this returns.  out_host (nullable): pinned host memory of B * (d + 1) doubles that
+ * receives [kg | dkg_dx], written by the envelope kernel itself (no copy after it); with out_host the
+ * call synchronises the stream and returns with the results in place (one host call per L-BFGS-B
+ * evaluation).  Same results, bit for bit, as dkg_plan_forward_grad on x_dev. */
 int dkg_plan_forward_grad_hostx(const void* host_plan, const void* dev_plan, const double* x_host, double* x_dev,
-                                int B, double* kg, double* dkg_dx, void* stream);
+                                int B, double* kg, double* dkg_dx, double* out_host, void* stream);
 /* Envelope sizes of the plan's last forward that was given kg_pairs (same B):
  * out[b*S + j] = the number of upper-envelope lines of pair (b, j), i.e. the
  * len(indices) of calculate_epigraph_indices (discretekg.py:341-412); 1 when the

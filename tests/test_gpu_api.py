@@ -177,14 +177,19 @@ def test_host_route_matches_device_route(B):
     assert acq(X[:0].unsqueeze(-2)).shape == (0,)
 
 
+@pytest.mark.parametrize("S", [8, 16, 24])
 @pytest.mark.parametrize("B", [1, 10, 11])
-def test_candidates_in_kernel_arguments_match_the_copy_path(B):
+def test_candidates_in_kernel_arguments_match_the_copy_path(B, S):
     """forward_grad_host with B * d <= DKG_XARG_MAX passes the candidates in the first kernel's arguments
-    (dkg_plan_forward_grad_hostx); past it, a pinned copy: both give dkg_plan_forward_grad's bits (d = 6:
-    B = 10 is inside, B = 11 past the bound)."""
+    (dkg_plan_forward_grad_hostx) and gets [KG | dKG/dx] written into its pinned buffer by the envelope
+    kernel (one workgroup per candidate at S = 8, the second of two at S = 16; copies after it at S = 24);
+    past the bound, a pinned copy in: all give dkg_plan_forward_grad's bits (d = 6: B = 10 is inside,
+    B = 11 past the bound)."""
     from dkg_amd import _lib
+    from dkg_amd.utils import sample_simplex
 
-    model, D, X, W = make_problem(WORKLOADS["parity6d"])
+    model, D, X, _ = make_problem(WORKLOADS["parity6d"])
+    W = sample_simplex(2, S, qmc=True, seed=5)
     acq = DiscreteKnowledgeGradient(model, D, W)
     plan = acq._plan_for(B, grad=True)
     assert (B * 6 <= _lib.DKG_XARG_MAX) == (B <= 10)

@@ -75,9 +75,9 @@ def test_validation_errors_without_device():
     # empty batch is a no-op
     assert lib.dkg_forward(outs, 1, 2, 16, 4, 16, 0, 16, 1, -1, 16, None, 16, 0, None) == _lib.DKG_OK
     # candidates in the kernel arguments: plan checks before any device work
-    assert lib.dkg_plan_forward_grad_hostx(None, None, None, None, 1, None, None, None) == _lib.DKG_ERR_ARG
+    assert lib.dkg_plan_forward_grad_hostx(None, None, None, None, 1, None, None, None, None) == _lib.DKG_ERR_ARG
     blank = ctypes.create_string_buffer(lib.dkg_plan_bytes())  # a plan never initialised: no DKG_PLAN_GRAD
-    st = lib.dkg_plan_forward_grad_hostx(blank, blank, None, None, 1, None, None, None)
+    st = lib.dkg_plan_forward_grad_hostx(blank, blank, None, None, 1, None, None, None, None)
     assert st == _lib.DKG_ERR_ARG and b"DKG_PLAN_GRAD" in lib.dkg_last_error()
 
 

@@ -83,6 +83,24 @@ for name, h2d, d2h in (("sync_only", False, False), ("h2d+sync", True, False), (
         stream.synchronize()
         ts.append(time.perf_counter() - t0)
     res[name] = med(ts)
+# the kernel-argument entry alone: without and with the pinned output written by the envelope kernel
+from dkg_amd import _lib  # noqa: E402
+lib = _lib.load()
+p1._host_buffers(w.d)
+xc = [x.cpu().contiguous() for x in xs]
+kgb = torch.empty(1, dtype=torch.double, device="cuda")
+dkgb = torch.empty(1, w.d, dtype=torch.double, device="cuda")
+outp = torch.empty(1 + w.d, dtype=torch.double).pin_memory()
+sptr = torch.cuda.current_stream().cuda_stream
+for name, hout in (("hostx+sync", 0), ("hostx+hout+sync", outp.data_ptr())):
+    ts = []
+    for i in range(calls):
+        t0 = time.perf_counter()
+        lib.dkg_plan_forward_grad_hostx(p1.host, p1._dev_ptr, xc[i].data_ptr(), dx.data_ptr(), 1, kgb.data_ptr(),
+                                        dkgb.data_ptr(), hout, sptr)
+        stream.synchronize()
+        ts.append(time.perf_counter() - t0)
+    res[name] = med(ts)
 # host overhead of the pieces alone
 ts = []
 for i in range(calls):
