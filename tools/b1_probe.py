@@ -130,6 +130,28 @@ for i in range(calls):
     ts.append(time.perf_counter() - t0)
 res["value_and_grad_host"] = med(ts)
 
+
+class _Trivial(torch.autograd.Function):  # the same autograd call shape with no device work: torch's own cost
+    @staticmethod
+    def forward(ctx, X, a):
+        ctx.save_for_backward(X)
+        return X.detach().sum(-1).reshape(X.shape[:-2])
+
+    @staticmethod
+    def backward(ctx, g):
+        (X,) = ctx.saved_tensors
+        return torch.ones_like(X), None
+
+
+ts = []
+for i in range(calls):
+    xa = xh[i].unsqueeze(-2).requires_grad_(True)
+    t0 = time.perf_counter()
+    loss = -_Trivial.apply(xa, None).sum()
+    (ga,) = torch.autograd.grad(loss, xa)
+    ts.append(time.perf_counter() - t0)
+res["autograd_floor_no_device"] = med(ts)
+
 ref = [p1.forward_grad(xs[i]) for i in range(8)]
 ref = [(a.cpu(), b.cpu()) for a, b in ref]
 if hasattr(p1, "forward_grad_host"):
