@@ -157,3 +157,29 @@ def test_not_positive_definite_raises():
     with pytest.raises(NotPSDError):
         run_prepare(st, max_tries=0)
     assert run_prepare(st, max_tries=1)[4] == pytest.approx(1e-8)
+
+
+def test_prepare_outputs_batched_matches_one_by_one():
+    """dkg_prepare_outputs (every output's factorisation in one chain, one status check, jitter retries per
+    failing output) gives each output's dkg_prepare_output results bit for bit: outputs of different n, a
+    kernel family each, one of them needing the first jitter retry."""
+    from dkg_amd.gp_state import prepare_outputs
+
+    g = torch.Generator().manual_seed(11)
+    X0 = torch.rand(37, 2, generator=g, dtype=torch.double)
+    Xj = torch.rand(12, 2, generator=g, dtype=torch.double)
+    Xj = torch.cat([Xj, Xj[:4]])  # duplicated inputs with a slightly negative shift: needs jitter
+    X2 = torch.rand(70, 2, generator=g, dtype=torch.double)
+    states = [SingleTaskGPState(X0, torch.randn(37, generator=g, dtype=torch.double), [0.3, 0.5], 2.0, 1e-3, 0.1,
+                                "matern", 2.5),
+              SingleTaskGPState(Xj, torch.randn(16, generator=g, dtype=torch.double), 0.5, 1.0, -5e-9, 0.0),
+              SingleTaskGPState(X2, torch.randn(70, generator=g, dtype=torch.double), [0.2, 0.9], 0.7, 1e-4, -0.3,
+                                "rbf")]
+    D = torch.rand(50, 2, generator=g, dtype=torch.double).to(DEV)
+    together = prepare_outputs(states, D)
+    for st, got in zip(states, together):
+        (alone,) = prepare_outputs([st], D)
+        assert got.jitter == alone.jitter
+        for name in ("L", "alpha", "root_frag", "disc_frag", "disc_mean"):
+            assert torch.equal(getattr(got, name), getattr(alone, name)), name
+    assert together[1].jitter == pytest.approx(1e-8) and together[0].jitter == 0.0 and together[2].jitter == 0.0
