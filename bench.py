@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--graph", type=int, default=2,
                     help="1 = replay each full exchange period (E forwards over the streams) as one captured HIP "
                          "graph; 2 = one single-stream graph per stream per period, replayed side by side")
+    ap.add_argument("--graph-head", type=int, default=1,
+                    help="--graph 2: each stream's period graph split into its first GRAPH_HEAD forwards and the rest, "
+                         "the heads of all streams launched first (0 = one graph per stream)")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")
     ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
     ap.add_argument("--nd-steps", type=int, default=256,
@@ -206,6 +209,7 @@ class Throughput:
         self.xchg = BatchExchange(B, E, mode, S_local=S_local, device=dev)
         self.main = torch.cuda.current_stream(dev)
         self.f32 = precision == "fp32"
+        self.head = 0
 
     def run(self, ns, steps, warmup, graph, world):
         E, xchg, main_s, dev = self.E, self.xchg, self.main, self.dev
@@ -237,22 +241,31 @@ class Throughput:
         if graph == 2 and steps >= E:
             # per stream one single-stream graph of its rows r = i mod ns: replayed on its own stream, each
             # enqueues its forwards as one batch (a graph forked over streams replays node by node)
+            # each stream's rows in two pieces, its first `head` forwards and the rest: the heads of all
+            # streams are launched first, so every stream has work a few us into the period instead of
+            # after the launches of the whole graphs before it (a launch costs ~1 us of host per kernel)
             for slot in range(2):
                 gs = []
                 for i in range(ns):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=streams[i] if i else torch.cuda.Stream(dev),
-                                          capture_error_mode="thread_local"):
-                        for r in range(i, E, ns):
-                            plans[i].forward_into(self.Xd, xchg.bufs[slot][r])
-                    gs.append(g)
+                    rows = list(range(i, E, ns))
+                    parts = [rows[:self.head], rows[self.head:]] if 0 < self.head < len(rows) else [rows]
+                    pieces = []
+                    for part in parts:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=streams[i] if i else torch.cuda.Stream(dev),
+                                              capture_error_mode="thread_local"):
+                            for r in part:
+                                plans[i].forward_into(self.Xd, xchg.bufs[slot][r])
+                        pieces.append(g)
+                    gs.append(pieces)
                 graphs.append(gs)
             torch.cuda.synchronize()
             # replayed with hipGraphLaunch on the raw executable graphs (what CUDAGraph.replay calls, without
             # its Python and stream-guard overhead: ~9 instead of ~18 us of host time per launch, which is
             # what a short run's four launches cost before the last stream starts)
             hip = hip_runtime()
-            execs = [[ctypes.c_void_p(g.raw_cuda_graph_exec()) for g in gs] for gs in graphs]
+            execs = [[[ctypes.c_void_p(g.raw_cuda_graph_exec()) for g in pieces] for pieces in gs] for gs in graphs]
+            npieces = max(len(p) for gs in graphs for p in gs)
             sptrs = [ctypes.c_void_p(s.cuda_stream) for s in streams]
             # the fork / join events, created once (torch's wait_stream creates an event per call)
             evs = [ctypes.c_void_p() for _ in range(ns)]
@@ -280,7 +293,8 @@ class Throughput:
             # one untimed replay of every graph (the first launch of a graph uploads it)
             for g in graphs:
                 for gi in (g if isinstance(g, list) else [g]):
-                    gi.replay()
+                    for gp in (gi if isinstance(gi, list) else [gi]):
+                        gp.replay()
             torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -305,8 +319,10 @@ class Throughput:
                         hip_check(hip.hipEventRecord(evs[0], sptrs[0]), "hipEventRecord")
                         for i in range(1, ns):
                             hip_check(hip.hipStreamWaitEvent(sptrs[i], evs[0], 0), "hipStreamWaitEvent")
-                    for i, ex in enumerate(execs[(k0 // E) % 2]):
-                        hip_check(hip.hipGraphLaunch(ex, sptrs[i]), "hipGraphLaunch")
+                    for p in range(npieces):
+                        for i, pieces in enumerate(execs[(k0 // E) % 2]):
+                            if p < len(pieces):
+                                hip_check(hip.hipGraphLaunch(pieces[p], sptrs[i]), "hipGraphLaunch")
                     for i in range(1, ns):
                         hip_check(hip.hipEventRecord(evs[i], sptrs[i]), "hipEventRecord")
                         hip_check(hip.hipStreamWaitEvent(sptrs[0], evs[i], 0), "hipStreamWaitEvent")
@@ -425,6 +441,7 @@ def main():
         E = max(1, min(args.exchange_every, args.steps))
         tp = Throughput(acq, X, w.B, E, "gather" if args.shard == "candidates" else "reduce", w.S, dev,
                         args.precision)
+        tp.head = args.graph_head
         return w, model, D, X0, W, acq, tp
 
     w, model, D, X0, W, acq, tp = setup(args.workload)
@@ -605,7 +622,9 @@ def main():
                                       f"per {E} forward batches",
                        "exchange_every": E, "streams": max(1, args.streams),
                        "hip_graph": {0: "off", 1: "one graph forked over the streams",
-                                     2: "one single-stream graph per stream"}.get(args.graph, str(args.graph))},
+                                     2: "one single-stream graph per stream"}.get(args.graph, str(args.graph))
+                       + (f" (first {args.graph_head} forward(s) of every stream launched first)"
+                          if args.graph == 2 and args.graph_head > 0 else "")},
             "host_launch_us_per_step": tp.host_us_per_step,
             "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,

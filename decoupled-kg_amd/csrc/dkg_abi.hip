@@ -152,7 +152,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   for (int i = 0; i < m; ++i)
     if (N > 0 && (!outs[i].disc_frag || !outs[i].disc_mean))
       return fail(DKG_ERR_ARG, "output %d: discretisation caches missing", i);
-  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK | DKG_PLAN_F32 | DKG_PLAN_FUSED))
+  if (flags & ~(DKG_PLAN_GRAD | DKG_PLAN_FORCE_WALK | DKG_PLAN_F32 | DKG_PLAN_FUSED | DKG_PLAN_NO_CHAIN))
     return fail(DKG_ERR_ARG, "unknown plan flags 0x%x", flags);
   if (want_grad && (flags & DKG_PLAN_F32))
     return fail(DKG_ERR_UNSUPPORTED, "the fp32 plan (DKG_PLAN_F32) is forward only; the gradient runs in fp64");
@@ -208,7 +208,8 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
   static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
   static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
-  P->debug_env = (denv ? std::atoi(denv) : 0) | ((flags & DKG_PLAN_FORCE_WALK) ? 1 : 0);
+  P->debug_env = (denv ? std::atoi(denv) : 0) | ((flags & DKG_PLAN_FORCE_WALK) ? 1 : 0) |
+                  ((flags & DKG_PLAN_NO_CHAIN) ? 8 : 0);
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
   static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
   P->debug_stamp = dst ? std::atoi(dst) : 0;

@@ -797,13 +797,13 @@ __device__ __forceinline__ bool chord_keep_reg(double b, double a, const double 
   return (a - a0) * db - (b - b0) * da >= -tau;
 }
 
-// One streaming round with NV = nv vertices (compile-time bound) read from LDS:
-// new vertices inserted into vb/va (lane 0), survivors of the 2(nv-1) chords
-// written to the list (capacity LIST_CAP_STREAM).  Returns the survivor count
-// (may exceed the capacity), or -1 if no line is above any chord.
+// Quickhull extension of a vertex chain (vb, va in LDS, nv <= NV vertices in increasing slope; lane 0 writes):
+// for every chord the line farthest above it (scaled height > 0; ties -> lowest line index) over the lines
+// build(ch, la, lb) gives for ch < nch, inserted after the chord's left end.  Returns the vertices found
+// (0: no line above any chord); nv and tpos (T's position) are updated.
 template <int MAXL, int NV, class Build>
-__device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* sb, double* sa, int* si, double* vb,
-                                            double* va, int& nv, int& tpos, Build&& build) {
+__device__ __forceinline__ int qh_extend(int nch, int nl, int lane, double* vb, double* va, int& nv, int& tpos,
+                                         Build&& build) {
   constexpr int NC = NV - 1;
   double vb_[NV], va_[NV];
 #pragma unroll
@@ -858,7 +858,7 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
       ba[cc] = a;
     }
   }
-  if (found == 0) return -1;
+  if (found == 0) return 0;
   // insert the new vertices (lane 0, from the back, as refine_list)
   if (lane == 0) {
     for (int i = nv - 1; i >= 0; --i) {
@@ -879,6 +879,17 @@ __device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* s
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return found;
+}
+
+// One streaming round with NV = nv vertices (compile-time bound) read from LDS:
+// new vertices inserted into vb/va (lane 0, qh_extend), survivors of the 2(nv-1)
+// chords written to the list (capacity LIST_CAP_STREAM).  Returns the survivor count
+// (may exceed the capacity), or -1 if no line is above any chord.
+template <int MAXL, int NV, class Build>
+__device__ __forceinline__ int stream_round(int nch, int nl, int lane, double* sb, double* sa, int* si, double* vb,
+                                            double* va, int& nv, int& tpos, Build&& build) {
+  if (qh_extend<MAXL, NV>(nch, nl, lane, vb, va, nv, tpos, build) == 0) return -1;
   // pass B: survivors of the new chords into the list
   constexpr int NV2 = 2 * NV - 1;
   const double Wb = vb[nv - 1] - vb[0];
@@ -1020,6 +1031,120 @@ __device__ __forceinline__ void stream_keep(const double (&la)[MAXL], const doub
       cnt += __popcll(mk);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Staged streaming forward, one pass (DKG_STG_SAMPLE): the survivor list is filtered against a chain of
+// lines of the set (the quickhull vertices of a strided sample of the pair's lines) instead of the chords
+// L-T / T-R of the exact extremes, which took a pass of their own.
+//
+// Why it is exact.  For a chain P_0 .. P_n of lines of the set with increasing slopes, the chord of P_c, P_c+1
+// is below the upper hull H of the whole set over [b_c, b_c+1] (H is concave and above every line), so
+// min_c ext_c(b) <= H(b) for every b in [b_0, b_n].  A line (a, b) is kept iff b < b_0, or b > b_n, or it is
+// within the margin tau_c of some chord's extension: fma(-s_c, b, a) >= K_c = fma(-s_c, b_c, a_c) - tau_c
+// (EnvChords' test and margin, W an upper bound of the set's slope range).  A line that fails every test lies
+// at least tau_c below H at its slope, so below the envelope by at least rel W everywhere: the guard argument
+// of DESIGN.md 4.3 holds for the walk over the list as for the two-chord list.  Every line of H (L, T, R
+// with their tie rules included) passes, so the list's own extremes are the set's.
+#ifndef DKG_STG_SAMPLE
+#define DKG_STG_SAMPLE 1
+#endif
+#ifndef DKG_SH_ROUNDS
+#define DKG_SH_ROUNDS 1
+#endif
+constexpr int SH_ROUNDS = DKG_SH_ROUNDS;  // quickhull rounds on the sample: 3 -> 5 (-> 9) vertices; one measured faster
+constexpr int SH_NC = SH_ROUNDS > 1 ? 8 : 4;     // chords of the chain
+
+template <int NC>
+struct ChainChords {
+  double s[NC], k[NC];
+  double blo, bhi;
+};
+
+// Keep tests of the chain (vb, va: nv lines of the set, increasing slope, in LDS) with the EnvChords margin;
+// W bounds the set's slope range.  Chords past the chain, or of zero width, keep nothing.
+template <int NC>
+__device__ __forceinline__ ChainChords<NC> chain_chords(const double* vb, const double* va, int nv, double W) {
+  ChainChords<NC> c;
+  c.blo = vb[0];
+  c.bhi = vb[nv - 1];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int i0 = min(i, nv - 1), i1 = min(i + 1, nv - 1);
+    const double b0 = vb[i0], a0 = va[i0], b1 = vb[i1], a1 = va[i1];
+    const double db = b1 - b0;
+    const double s = (i + 1 < nv && db > 0.0) ? (a1 - a0) / db : 0.0;
+    const double tau = WALK_MARGIN * (fmax(fabs(a0), fabs(a1)) + fabs(s) * (fmax(fabs(b0), fabs(b1)) + W) + W);
+    c.s[i] = s;
+    c.k[i] = (i + 1 < nv && db > 0.0) ? fma(-s, b0, a0) - tau : INFINITY;
+  }
+  return c;
+}
+
+// The chain filter of one staged chunk (lines base + lane + 64 t) into the wave's long list (LIST_CAP_STREAM
+// entries; cnt counts on past it).
+template <int MAXL, int NC>
+__device__ __forceinline__ void chain_keep(const double (&la)[MAXL], const double (&lb)[MAXL], int base, int nl,
+                                           const ChainChords<NC>& c, int lane, double* sb, double* sa, int* si,
+                                           int& cnt) {
+  // the keep masks of a group of four slots first (independent tests, no branch between them), then the
+  // group's writes (rarely any)
+#pragma unroll
+  for (int t0 = 0; t0 < MAXL; t0 += 4) {
+    uint64_t mk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u;
+      if (t < MAXL) {
+        const double a = la[t], b = lb[t];
+        bool s = (b < c.blo) | (b > c.bhi);
+#pragma unroll
+        for (int i = 0; i < NC; ++i) s = s | (fma(-c.s[i], b, a) >= c.k[i]);
+        mk[u] = ballot(s & (base + lane + 64 * t < nl));
+      } else {
+        mk[u] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u;
+      if (t < MAXL && mk[u] != 0) {  // wave-uniform, rarely taken
+        if ((mk[u] >> lane) & 1) {
+          const int pos = cnt + lanes_below(mk[u]);
+          if (pos < LIST_CAP_STREAM) {
+            sb[pos] = lb[t];
+            sa[pos] = la[t];
+            si[pos] = base + lane + 64 * t;
+          }
+        }
+        cnt += __popcll(mk[u]);
+      }
+    }
+  }
+}
+
+// L, T, R (with the tie rules of ext_fold) and the short-circuit status of the cnt lines of a survivor list.
+__device__ __forceinline__ FwdEnv list_extremes(int cnt, int lane, const double* sb, const double* sa) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  ExtAcc e;
+  for (int q = 0; 64 * q < cnt; ++q) {
+    const int i = lane + 64 * q;
+    const bool live = i < cnt;
+    const int ii = live ? i : 0;
+    const double a = sa[ii], b = sb[ii];
+    const bool l = live & ((b < e.bmin) | ((b == e.bmin) & (a > e.aLx)));
+    e.bmin = l ? b : e.bmin;
+    e.aLx = l ? a : e.aLx;
+    const bool r = live & ((b > e.bmax) | ((b == e.bmax) & (a > e.aRx)));
+    e.bmax = r ? b : e.bmax;
+    e.aRx = r ? a : e.aRx;
+    const bool tt = live & ((a > e.amax) | ((a == e.amax) & (b < e.bTx)));
+    e.amax = tt ? a : e.amax;
+    e.bTx = tt ? b : e.bTx;
+  }
+  return ext_reduce(e);
 }
 
 // After the extremes and the filter pass (cnt survivors in the list): quickhull rounds if the list
@@ -1502,6 +1627,89 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
         lb[0] = (lane == 0) ? bb0 : lb[0];
       }
     };
+#if DKG_STG_SAMPLE
+    // pass 0: the pair's sample hull.  Every stride-th line (line j * stride in slot j of a staged chunk laid
+    // out as chunk 0) staged in buffer 0 by one strided DMA, then per wave the sample's extremes and
+    // SH_ROUNDS quickhull rounds in registers; the vertex chain (lines of the set) goes to buffer 1.
+    const int stride = (NL + SCH - 1) / SCH;
+    {
+      constexpr int NP2 = MP / 2, GR = SCH / 64, NI = NP2 * GR;
+      for (int ii = wave; ii < 2 * NI; ii += SW) {
+        const int arr = ii / NI, rem = ii % NI, q2 = rem / GR, gi = rem % GR;
+        const double* src = arr ? cvb : mu_all;
+        const int rec = min(max((gi * 64 + lane_k) * stride - 1, 0), N - 1);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (size_t)rec * MP + 2 * q2),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(cbuf + (size_t)arr * CBL +
+                                                                         ((size_t)q2 * SCH + gi * 64) * 2)),
+                                         16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ChainChords<SH_NC> cc;
+    bool chain_ok = false;
+    // test hook (DKG_PLAN_NO_CHAIN): no chain, every pair takes the overflow path
+    if (has && !(__builtin_amdgcn_readfirstlane(P->debug_env) & 8)) {
+      double la[CS], lb[CS];
+      build_staged(0, la, lb);  // sample line j in slot j (q = 0: line 0 from registers; j * stride > N: a copy
+                                // of line N, still a line of the set)
+      ExtAcc es;
+      ext_fold<CS>(la, lb, 0, SCH, lane, es);
+      const FwdEnv fs = ext_reduce(es);
+      double* vb = cbuf + 2 * (size_t)CBL + (size_t)wave * VREG;
+      double* va = vb + VCAP;
+      if (fs.status == 0) {
+        if (lane == 0) {
+          vb[0] = fs.bL; va[0] = fs.aL;
+          vb[1] = fs.bT; va[1] = fs.aT;
+          vb[2] = fs.bR; va[2] = fs.aR;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int nv = 3, tpos = 1;
+        auto sample = [&](int, double (&xa)[CS], double (&xb)[CS]) {
+#pragma unroll
+          for (int t = 0; t < CS; ++t) { xa[t] = la[t]; xb[t] = lb[t]; }
+        };
+        if (qh_extend<CS, 3>(1, SCH, lane, vb, va, nv, tpos, sample) > 0 && SH_ROUNDS > 1)
+          qh_extend<CS, 5>(1, SCH, lane, vb, va, nv, tpos, sample);
+        // the set's slope range is at most 2 sum_i |wb_i| sqrt(v_i(x) s_i) (Cauchy-Schwarz on the posterior
+        // covariance, the posterior variance at z below the prior s_i), with room for the rounding of cov
+        double bm = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          bm = fma(fabs(wb[i]), sqrt(fmax(sv[i], 0.0) * fmax(os[i], 0.0)) + 1e-8 * fabs(os[i]), bm);
+        cc = chain_chords<SH_NC>(vb, va, nv, 2.0 * bm * (1.0 + 1e-6));
+        chain_ok = true;
+      }
+    }
+    __syncthreads();  // every wave has its chain in registers: the buffers take the staged chunks
+#ifdef DKG_STG_STAMPS
+    if (st) st[4] = __builtin_amdgcn_s_memtime();  // pass 0 done
+#endif
+    // the staged pass: the chain filter into the survivor list
+    stage(0);
+    for (int q = 0; q < nq; ++q) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (q + 1 < nq) stage(q + 1);
+      if (chain_ok) {
+        double la[CS], lb[CS];
+        build_staged(q, la, lb);
+        chain_keep<CS, SH_NC>(la, lb, q * SCH, NL, cc, lane, sb, sa, sif, scnt);
+      }
+    }
+    __syncthreads();  // the chunk buffers are the refinement's vertex arrays from here
+#ifdef DKG_STG_STAMPS
+    if (st) st[5] = __builtin_amdgcn_s_memtime();  // staged pass done
+#endif
+    // no chain (the sample has a single slope): the per-pair tail takes the extremes and the filter from the
+    // streamed lines (overflow path)
+    if (!chain_ok) scnt = LIST_CAP_STREAM + 1;
+    sf.status = 0;
+#else
     // pass 1: extremes
     ExtAcc e;
 #ifdef DKG_STG_STAMPS
@@ -1549,6 +1757,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     if (st) st[4] = twait;  // raw: wait cycles of wave 0 over both passes
     if (st) st[5] = __builtin_amdgcn_s_memtime();
 #endif
+#endif  // DKG_STG_SAMPLE
   }
 #undef STG_W0
 #undef STG_W1
@@ -1933,6 +2142,15 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
       if (lane == 0)
         for (int dd = 0; dd < d; ++dd) gw[dd] = 0.0;
     } else if constexpr (STG) {
+#if DKG_STG_SAMPLE
+      // L, T, R and the short-circuit test from the list (it holds every upper-hull line of the set), or,
+      // after an overflow, from the streamed lines
+      sf = (scnt <= LIST_CAP_STREAM) ? list_extremes(scnt, lane, sb, sa) : env_extremes_stream<MAXL>(nch, NL, lane,
+                                                                                                     build_chunk);
+#ifdef DKG_STG_STAMPS
+      if (lane == 0) P->hull_pairs[(size_t)b * S + j] = scnt;  // diagnostics build: the list length per pair
+#endif
+#endif
       if (sf.status == 1) {
         kgj = 0.0;
         hn = 1;
@@ -1954,7 +2172,11 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     }
     if (pairs_out != nullptr && lane == 0) {
       pairs_out[(size_t)b * S + j] = kgj;
+#ifdef DKG_STG_STAMPS
+      if constexpr (!GRAD && !STG) P->hull_pairs[(size_t)b * S + j] = hn;  // STG: the list length, above
+#else
       if constexpr (!GRAD) P->hull_pairs[(size_t)b * S + j] = hn;
+#endif
     }
     if (lane == 0) skg[j - j0] = kgj;
   }

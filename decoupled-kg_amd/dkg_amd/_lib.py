@@ -23,6 +23,7 @@ DKG_PLAN_GRAD = 1
 DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
 DKG_PLAN_F32 = 4  # fp32 contractions (BASELINE configs[4]); forward only
 DKG_PLAN_FUSED = 8  # the forward as one launch with in-launch hand-offs (dkg_fused.h); not the default
+DKG_PLAN_NO_CHAIN = 16  # test hook: the streaming envelope's list-overflow path (no sample chain) for every pair
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 

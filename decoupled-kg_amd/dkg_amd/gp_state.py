@@ -147,8 +147,8 @@ class DeviceGPState:
         self._ws_key = None
 
     def plan(self, W: torch.Tensor, target, max_B: int, grad: bool = False, force_walk: bool = False,
-             f32: bool = False, fused: bool = False) -> "ForwardPlan":
-        return ForwardPlan(self, W, target, max_B, grad, force_walk, f32, fused)
+             f32: bool = False, fused: bool = False, no_chain: bool = False) -> "ForwardPlan":
+        return ForwardPlan(self, W, target, max_B, grad, force_walk, f32, fused, no_chain)
 
     def forward(self, X: torch.Tensor, W: torch.Tensor, target, kg_pairs=None, timed: bool = False):
         """One-shot forward (builds a plan on the fly); see ForwardPlan for the fast path."""
@@ -166,7 +166,7 @@ class ForwardPlan:
     dKG/dx alongside KG."""
 
     def __init__(self, state: DeviceGPState, W: torch.Tensor, target, max_B: int, grad: bool = False,
-                 force_walk: bool = False, f32: bool = False, fused: bool = False):
+                 force_walk: bool = False, f32: bool = False, fused: bool = False, no_chain: bool = False):
         lib = _lib.load()
         self.state = state
         self.device = state.device
@@ -182,7 +182,8 @@ class ForwardPlan:
         self.grad = bool(grad)
         self.f32 = bool(f32)
         flags = ((_lib.DKG_PLAN_GRAD if self.grad else 0) | (_lib.DKG_PLAN_FORCE_WALK if force_walk else 0)
-                 | (_lib.DKG_PLAN_F32 if self.f32 else 0) | (_lib.DKG_PLAN_FUSED if fused else 0))
+                 | (_lib.DKG_PLAN_F32 if self.f32 else 0) | (_lib.DKG_PLAN_FUSED if fused else 0)
+                 | (_lib.DKG_PLAN_NO_CHAIN if no_chain else 0))
         need = lib.dkg_plan_workspace(state.structs, state.m, state.d, state.N, self.max_B, self.S, flags)
         self.ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
         nbytes = lib.dkg_plan_bytes()

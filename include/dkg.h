@@ -185,6 +185,10 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
  * MI355X an in-launch hand-off costs about what the kernel boundary it replaces
  * does, and the early-dispatched consumers slow the producers. */
 #define DKG_PLAN_FUSED 8
+/* DKG_PLAN_NO_CHAIN (test hook): the streaming envelope (N + 1 > 2112 lines, or line data beyond LDS)
+ * filters without its sample chain: the extremes from the streamed lines, the quickhull refinement and
+ * the walks of the list-overflow path for every pair; same results, slower. */
+#define DKG_PLAN_NO_CHAIN 16
 size_t dkg_plan_bytes(void);
 size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags);
 int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int N, const double* weights, int S,

@@ -350,13 +350,34 @@ def test_stress_config_parity(target):
 
 @pytest.mark.parametrize("target", [None, 1])
 def test_stress_refinement_parity(target):
-    """Streaming envelope at the stress shape over 24 candidates x 32 scalarisations: long candidate
-    lists (the stress lines keep up to ~2000 of 4097 lines near the chords L-T / T-R) go through the
-    streamed quickhull rounds before the walk."""
+    """Streaming envelope at the stress shape over 24 candidates x 32 scalarisations (noise 1e-3 s: many
+    lines near the upper hull; the sample chain keeps up to a few hundred of the 4097 lines per pair)."""
     from dkg_amd.synthetic import WORKLOADS, make_problem
 
     model, D, X, W = make_problem(WORKLOADS["stress32"])
     check_parity_case(parity_case(model, D, W, X[:24], target))
+
+
+@pytest.mark.parametrize("workload,target", [("stress32", None), ("stress", 2)])
+def test_stress_sample_chain_matches_overflow_path(workload, target):
+    """The streaming envelope's one staged pass filters against the chain of a strided sample's quickhull
+    vertices (dkg_device.h chain_keep); DKG_PLAN_NO_CHAIN sends every pair through the overflow path
+    instead (extremes from the streamed lines, quickhull refinement, the walks).  Both walks are the
+    reference walk, so KG per pair and the envelope sizes must agree bit for bit."""
+    from dkg_amd import DiscreteKnowledgeGradient
+    from dkg_amd.synthetic import WORKLOADS, make_problem
+
+    model, D, X, W = make_problem(WORKLOADS[workload])
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    Xd = X[:32].to(DEV).contiguous()
+    chain = acq._state.plan(acq._W, acq._target, 32)
+    plain = acq._state.plan(acq._W, acq._target, 32, no_chain=True)
+    kg_c, pairs_c, hull_c = chain.forward_stats(Xd)
+    kg_p, pairs_p, hull_p = plain.forward_stats(Xd)
+    assert int((pairs_c > 0).sum()) > 0
+    assert torch.equal(pairs_c, pairs_p)
+    assert torch.equal(hull_c, hull_p)
+    assert torch.equal(kg_c, kg_p)
 
 
 # ---------------------------------------------------------------- fp32 contractions (DKG_PLAN_F32)

@@ -40,3 +40,12 @@ print("passes      ", q(passes))
 print("  waiting   ", q(wait))
 print("  computing ", q(passes - wait))
 print("tail (refine/walk/sum)", q(tail))
+if os.environ.get("DKG_STG_SAMPLE", "1") != "0":
+    # sample-hull build: slot 4 = pass 0 (sample hull) done, slot 5 = the staged pass done; hull sizes hold
+    # the list lengths
+    p0 = st[:, 4] - st[:, 3]
+    print("pass 0 (sample hull)", q(p0))
+    print("staged pass         ", q(st[:, 5] - st[:, 4]))
+    _, _, cnt = plan.forward_stats(Xd)
+    c = cnt.flatten().cpu().numpy().astype(np.int64)
+    print("list length          ", q(c), "over 512:", int((c > 512).sum()), "of", c.size)
