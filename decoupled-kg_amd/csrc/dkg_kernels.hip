@@ -339,6 +339,15 @@ hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s) {
   }
 }
 
+// The 64 x 64 covariance blocks (posterior_cov_wide_kernel) when they still give every CU two blocks
+// (e.g. the stress shape: 768 blocks); smaller batches keep the 32 x 32 blocks, whose latency is what
+// sets a short forward.  DKG_COV_WIDE=0 / 1 (A/B measurements) forces the choice.
+static bool cov_wide(int N, int B, int m) {
+  static const char* env = std::getenv("DKG_COV_WIDE");
+  if (env) return std::atoi(env) != 0 && N >= 64 && B >= 64;
+  return N >= 64 && B >= 64 && (size_t)((N + 63) / 64) * ((B + 63) / 64) * m >= 512;
+}
+
 template <int DM, class T>
 static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
                                       hipStream_t s, int stage) {
@@ -349,6 +358,14 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
     hipLaunchKernelGGL((cross_root_plan_kernel<DM, T>), grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
                        h.debug_stamp);
     return hipGetLastError();
+  }
+  if constexpr (sizeof(T) == 8 && DM <= 4) {
+    if (cov_wide(h.N, B, h.m)) {
+      dim3 grid((h.N + 63) / 64, (B + 63) / 64, h.m);
+      hipLaunchKernelGGL((posterior_cov_wide_kernel<DM>), grid, dim3(PW_WAVES * WAVE), 0, s, dev, xnew, B,
+                         h.debug_stamp);
+      return hipGetLastError();
+    }
   }
   dim3 grid(std::max(1, (h.N + 31) / 32), (B + 16 * PC_RB - 1) / (16 * PC_RB), h.m);
   hipLaunchKernelGGL((posterior_cov_kernel<DM, T>), grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B, h.debug_stamp);

@@ -478,6 +478,130 @@ __device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, c
   KST_END(st);
 }
 
+// ---------------------------------------------------------------------------
+// posterior_cov_wide_kernel (fp64, d <= 4, large B x N, e.g. BASELINE configs[4]): the same covariance rows from
+// 64 x 64 blocks.  At 32 x 32 every operand byte feeds 32 flops: the stress shape's 3072 blocks read
+// 1.5 GB of Q_X / Q_D tiles through L2 and the MALL (Q_D 96 MB), about what the MFMAs take.  Here wave w
+// computes a 2 x 2 group of 16 x 16 tiles (row half (w & 3) >> 1, column half w & 1) over K part w >> 2:
+// every 16-byte operand load feeds four MFMAs instead of two, and a block reads half the bytes per flop.
+// The parts meet in LDS, each finalising one row tile of its group (deterministic: a sum of two commutes);
+// the kernel terms of the 8 outputs per lane are evaluated there and stored.  One
+// accumulator per tile (posterior_cov_kernel keeps four per tile, by k-block mod 4), so the sums agree
+// with it to rounding, not bit for bit.
+constexpr int PW_WAVES = 8;
+constexpr int PW_KS = 2;  // K parts
+constexpr int PW_P = 4;   // 16-byte words per operand tile per load batch
+
+template <int DM>
+__global__ __launch_bounds__(PW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(4))) void posterior_cov_wide_kernel(const Plan* __restrict__ P,
+                                                                             const double* __restrict__ xnew,
+                                                                             int B, int dst) {
+  __shared__ __attribute__((aligned(16))) double part[2 * 4 * 2 * 4 * 64];  // [row tile][sub-block][col tile] sums
+  __shared__ double qpart[2 * 4 * 16];                                      // [row tile][sub-block] |Q_X|^2 sums
+  unsigned long long* st = kst_slot(dst, P, 1);
+  KST_BEGIN(st);
+  const int oi = blockIdx.z;
+  const dkg_output& o = P->o[oi];
+  const int N = P->N;
+  const int d = P->d;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sb = wave & 3, ks = wave >> 2;
+  const int ti0 = 4 * blockIdx.y + 2 * (sb >> 1);  // row tiles ti0, ti0 + 1
+  const int tk0 = 4 * blockIdx.x + 2 * (sb & 1);   // column tiles tk0, tk0 + 1
+  const int RT = pad16(B) / 16, CT = pad16(N) / 16;  // tiles that exist
+  const int KB = pad16(o.n) / 4;
+  const int KP = KB / 2;  // 16-byte words (two k-blocks each)
+  const int KPs = (KP + PW_KS - 1) / PW_KS;
+  const int p0 = min(KP, ks * KPs), p1 = min(KP, p0 + KPs);
+  const double* qx = P->q[oi];
+  const double* qd = o.disc_frag;
+  // dead tiles read a live one (results discarded)
+  const int tr[2] = {min(ti0, RT - 1), min(ti0 + 1, RT - 1)};
+  const int tc[2] = {min(tk0, CT - 1), min(tk0 + 1, CT - 1)};
+  const bool want_var = (tk0 == 0);  // this wave's column tiles include tile 0: the row tiles' variances
+  double va[PW_P][2][2], vd[PW_P][2][2];
+  auto load_batch = [&](int pb) {
+#pragma unroll
+    for (int u = 0; u < PW_P; ++u) {
+      const int j = min(pb + u, p1 - 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        frag_word<double>(qx, tr[h], j, lane, KB, va[u][h]);
+        frag_word<double>(qd, tc[h], j, lane, KB, vd[u][h]);
+      }
+    }
+  };
+  if (p0 < p1) load_batch(p0);
+  KST(st, 2);
+  d4 acc[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  double qsq[2] = {0.0, 0.0};  // lane l: this wave's sum of Q_X[16 tr[h] + (l & 15)][k]^2
+  for (int pb = p0; pb < p1; pb += PW_P) {
+    if (pb != p0) load_batch(pb);
+#pragma unroll
+    for (int u = 0; u < PW_P; ++u) {
+      const bool in = pb + u < p1;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+#pragma unroll
+        for (int hr = 0; hr < 2; ++hr) {
+          const double a = va[u][hr][q];
+#pragma unroll
+          for (int hc = 0; hc < 2; ++hc) acc[hr][hc] = mfma_f64(a, in ? vd[u][hc][q] : 0.0, acc[hr][hc]);
+          if (want_var) qsq[hr] = in ? fma(a, a, qsq[hr]) : qsq[hr];
+        }
+      }
+    }
+  }
+  KST(st, 3);
+  if (want_var) {
+#pragma unroll
+    for (int hr = 0; hr < 2; ++hr) {
+      qsq[hr] += __shfl_xor(qsq[hr], 16);
+      qsq[hr] += __shfl_xor(qsq[hr], 32);
+    }
+  }
+  // The two K parts exchange halves: part ks finalises row tile hr = ks of its 2 x 2 group and hands the
+  // other row tile's sums to the other part (LDS), so both halves of the workgroup share the epilogue.
+  {
+    const int ho = 1 - ks;  // the row tile handed over
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(((ho * 4 + sb) * 2 + hc) * 4 + r) * 64 + lane] = acc[ho][hc][r];
+    if (want_var && lane < 16) qpart[(ho * 4 + sb) * 16 + lane] = qsq[ho];
+  }
+  __syncthreads();
+  KST(st, 4);
+  {
+    // the kernel terms s k(x_b, D_k) here, after the contraction: held across it they took the block
+    // past 128 VGPRs (one block per CU instead of two)
+    const int hr = ks;
+    const int rec = cov_rec(P->m);
+    const double os = o.outputscale;
+    const int kind = o.kernel;
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc) {
+      const int k = 16 * (tk0 + hc) + (lane & 15);
+      const double* xk = P->disc + (size_t)min(k, max(N, 1) - 1) * d;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // K part 0 + K part 1 (fp addition commutes: the same bits whichever part adds)
+        const double sum = acc[hr][hc][r] + part[(((hr * 4 + sb) * 2 + hc) * 4 + r) * 64 + lane];
+        const int b = 16 * (ti0 + hr) + mfma_drow<double>(lane, r);
+        const double kv =
+            os * kernel_profile(kind, scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d));
+        if (b < B && k < N) P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kv - sum;
+      }
+    }
+    if (want_var && lane < 16) {
+      const int bb = 16 * (ti0 + hr) + lane;
+      if (bb < B) P->var[oi][bb] = o.outputscale - (qsq[hr] + qpart[(hr * 4 + sb) * 16 + lane]);
+    }
+  }
+  KST_END(st);
+}
+
 template <int DM, class T = double>
 __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
                                                                          const double* __restrict__ xnew, int B,
