@@ -40,6 +40,7 @@ struct WsLayout {
   size_t qxrm[DKG_MAX_OUTPUTS];
   size_t qdrm[DKG_MAX_OUTPUTS];
   size_t q[DKG_MAX_OUTPUTS];
+  size_t kx[DKG_MAX_OUTPUTS];  // 0: none (cross_kfill off for this output)
   size_t q32[DKG_MAX_OUTPUTS], root32[DKG_MAX_OUTPUTS], disc32[DKG_MAX_OUTPUTS];
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
@@ -50,6 +51,12 @@ struct WsLayout {
   size_t hull_pairs;
   size_t total;
 };
+
+static int max_np_of(const dkg_output* outs, int m) {
+  int np = 0;
+  for (int i = 0; i < m; ++i) np = std::max(np, pad16(outs[i].n));
+  return np;
+}
 
 WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, int flags = 0) {
   WsLayout L{};
@@ -71,6 +78,11 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
     }
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
+    L.kx[i] = 0;
+    if (cross_kfill(max_np_of(outs, m))) {  // the launch covers every output of the plan
+      L.kx[i] = off;
+      off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
+    }
     if (flags & DKG_PLAN_F32) {
       const size_t np = pad16(outs[i].n);
       L.q32[i] = off;
@@ -189,6 +201,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
       P->qdrm[i] = reinterpret_cast<double*>(ws + L.qdrm[i]);
     }
     P->q[i] = reinterpret_cast<double*>(ws + L.q[i]);
+    P->kx[i] = L.kx[i] ? reinterpret_cast<double*>(ws + L.kx[i]) : nullptr;
     if (flags & DKG_PLAN_F32) {
       P->q32[i] = reinterpret_cast<float*>(ws + L.q32[i]);
       P->root32[i] = reinterpret_cast<float*>(ws + L.root32[i]);

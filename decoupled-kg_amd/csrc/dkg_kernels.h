@@ -23,6 +23,16 @@ __host__ __device__ constexpr int cov_rec(int m) { return m <= 1 ? 1 : m <= 2 ? 
 // (written once per (model, discretisation, weights) by dkg_plan_init): the
 // kernels take a pointer to it, so each launch carries ~40 bytes of arguments
 // instead of a ~1 KiB by-value block (measured ~1.5 us of launch cost).
+// Large n: K(x, X) is filled once per forward by its own kernel (cross_kfill_kernel) and the cross
+// workgroups load their slab of it.  Every column-pair group of a row tile otherwise evaluates the
+// kernel over the columns its wider tile needs: at n = 1024 (64 tiles, 32 groups) each entry ~24 times,
+// which took most of the stage.  At the headline's n = 256 the extra launch costs more than it saves
+// (profiles/r02/r02zz).
+#ifndef DKG_CROSS_KFILL
+#define DKG_CROSS_KFILL 1
+#endif
+__host__ __device__ inline bool cross_kfill(int np) { return DKG_CROSS_KFILL && np >= 512; }
+
 struct Plan {
   dkg_output o[DKG_MAX_OUTPUTS];
   int32_t m, d, N, S, target;       // target < 0: all outputs observed
@@ -37,6 +47,8 @@ struct Plan {
   const double* disc;               // [N x d]
   const double* weights;            // [S x m]
   double* q[DKG_MAX_OUTPUTS];       // fragment-packed K(x, X) R per output (workspace)
+  double* kx[DKG_MAX_OUTPUTS];      // large n (cross_kfill): K(x, X) per output in the cross stage's B-operand
+                                    // order [B_pad / 16][n_pad / 4][64], filled once per forward (else null)
   double* mux[DKG_MAX_OUTPUTS];     // posterior mean at the candidates per output (workspace)
   double* var[DKG_MAX_OUTPUTS];     // noiseless posterior variance s - |Q_X[b]|^2 per output (workspace)
   double* jq[DKG_MAX_OUTPUTS];      // GRAD: J_g = dK(x,X)/dx_g R, row-major [d][bpad][n_pad] per output

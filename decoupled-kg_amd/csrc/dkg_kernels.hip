@@ -93,11 +93,21 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
   }
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 2)) return;  // ablation: empty cross stage
   if constexpr (sizeof(T) == 8) {
-    cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st);
+    cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st, 0,
+                        P->kx[oi]);
   } else {
     cross_root_impl<DM, false, float>(P->o[oi], P->d, xnew, B, P->q32[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem,
-                                      st, 0, nullptr, nullptr, P->root32[oi]);
+                                      st, 0, P->kx[oi], nullptr, P->root32[oi]);
   }
+}
+
+// K(x, X) for the cross stage of large n (cross_kfill): grid (B tiles, k-block groups of KF_KB, outputs).
+template <int DM>
+__global__ __launch_bounds__(KF_WAVES * WAVE) void cross_kfill_kernel(const Plan* __restrict__ P,
+                                                                     const double* __restrict__ xnew, int B) {
+  const int oi = blockIdx.z;
+  if (P->kx[oi] == nullptr) return;
+  cross_kfill_body<DM>(P->o[oi], P->d, xnew, B, P->kx[oi], blockIdx.x, blockIdx.y * KF_KB);
 }
 
 // Value + gradient cross stage, one launch: grid (B tiles, pairs, m + m d).
@@ -352,6 +362,10 @@ template <int DM, class T>
 static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
                                       hipStream_t s, int stage) {
   if (stage == 0) {
+    if (h.kx[0] != nullptr) {
+      dim3 kgrid(pad16(B) / 16, (h.max_np / 4 + KF_KB - 1) / KF_KB, h.m);
+      hipLaunchKernelGGL((cross_kfill_kernel<DM>), kgrid, dim3(KF_WAVES * WAVE), 0, s, dev, xnew, B);
+    }
     dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
     raise_lds_limit((const void*)cross_root_plan_kernel<DM, T>, lds);

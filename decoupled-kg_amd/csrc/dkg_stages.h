@@ -78,6 +78,61 @@ __host__ __device__ inline int cross_pairs(int np, int d) {
 __host__ __device__ inline int cross_groups(int np, int d) {
   return ((np / 16 + 1) / 2 + cross_pairs(np, d) - 1) / cross_pairs(np, d);
 }
+constexpr int KF_WAVES = 4;
+constexpr int KF_KB = 16;  // k-blocks (of 4 columns) per fill workgroup
+
+// Pre-scaled r^2 and the kernel term exactly as cross_root_impl's fill evaluates them (same operations,
+// same order), so a loaded entry is the bits the fill would have produced.
+template <int DM, int KIND>
+__device__ __forceinline__ double cross_kernel_term(const double (&xr)[DM], const double* __restrict__ xs_col, int d,
+                                                    double os, const_dptr tab) {
+  double r2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    const double t = xr[k] - xs_col[min(k, d - 1)];
+    r2 = fma(t, (k < d) ? t : 0.0, r2);
+  }
+  return os * kernel_profile_t<KIND>(r2, tab);
+}
+
+// K(x_b, X_j) of output o for a row tile ti and KF_KB k-blocks, in the cross stage's B-operand order
+// (element e = kb * 64 + l: row 16 ti + (l & 15), column 4 kb + (l >> 4)); zero outside B x n.
+template <int DM>
+__device__ __forceinline__ void cross_kfill_body(const dkg_output& o, int d, const double* __restrict__ x, int rows,
+                                                 double* __restrict__ kx, int ti, int kb0) {
+  const int n = o.n;
+  const int KB = pad16(n) / 4;
+  const int lane = threadIdx.x & 63;
+  const int row = ti * 16 + (lane & 15);
+  const bool rv = row < rows;
+  const int rowc = min(row, rows - 1);
+  double xr[DM];
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    const int kk = min(k, d - 1);
+    xr[k] = x[(size_t)rowc * d + kk] * o.inv_lengthscale[kk];
+  }
+  const double os = o.outputscale;
+  auto fill = [&](auto kind_c) {
+    constexpr int KIND = decltype(kind_c)::value;
+    const const_dptr tab = psi_tab();
+    for (int kb = kb0 + (int)(threadIdx.x >> 6); kb < min(KB, kb0 + KF_KB); kb += KF_WAVES) {
+      const int col = 4 * kb + (lane >> 4);
+      const int cc = min(col, n - 1);
+      double xs[DM];
+#pragma unroll
+      for (int k = 0; k < DM; ++k) xs[k] = o.train_x[(size_t)cc * d + min(k, d - 1)] * o.inv_lengthscale[min(k, d - 1)];
+      const double kv = cross_kernel_term<DM, KIND>(xr, xs, d, os, tab);
+      kx[((size_t)ti * KB + kb) * 64 + lane] = (rv && col < n) ? kv : 0.0;
+    }
+  };
+  switch (o.kernel) {
+    case DKG_MATERN12: fill(std::integral_constant<int, DKG_MATERN12>{}); break;
+    case DKG_MATERN32: fill(std::integral_constant<int, DKG_MATERN32>{}); break;
+    case DKG_RBF: fill(std::integral_constant<int, DKG_RBF>{}); break;
+    default: fill(std::integral_constant<int, DKG_MATERN52>{}); break;
+  }
+}
 
 // WT: the forward's Q_X / mean stores write-through (sc1), for the fused forward's hand-off (st_out).
 // GRAD: the same contraction with the kernel replaced by its derivative in
@@ -89,9 +144,10 @@ template <int DM, bool GRAD = false, class ET = double, bool WT = false>
 __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, const double* __restrict__ x, int rows,
                                                 ET* __restrict__ qout, double* __restrict__ mout, int ti, int grp,
                                                 double* smem, unsigned long long* st = nullptr, int gdim = 0,
-                                                const double* __restrict__ /*unused*/ = nullptr,
+                                                const double* __restrict__ kx = nullptr,
                                                 double* __restrict__ qx_rm = nullptr,
                                                 const ET* __restrict__ root = nullptr) {
+  // kx (forward, large n): K(x, X) of this output filled by cross_kfill_kernel, loaded instead of evaluated
   static_assert(!GRAD || sizeof(ET) == 8, "the gradient stage is fp64");
   constexpr int QW = kpack<ET>();
   if constexpr (sizeof(ET) == 8) root = o.root_frag;
@@ -150,7 +206,8 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
   const bool want_mean = (mout != nullptr) && (pb == 0);  // pair 0 covers every column
   // training inputs staged pre-scaled by 1/lengthscale (GPyTorch divides both
   // inputs by the lengthscale before the distance)
-  for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e] * o.inv_lengthscale[e % d];
+  if (kx == nullptr)
+    for (int e = tid; e < ncol * d; e += CR_WAVES * WAVE) xs[e] = o.train_x[e] * o.inv_lengthscale[e % d];
   if (want_mean)
     for (int e = tid; e < ncol; e += CR_WAVES * WAVE) als[e] = o.alpha[e];
   const int row = ti * 16 + (lane & 15);
@@ -183,17 +240,19 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       const int e = tid + it * CR_WAVES * WAVE;
       const int col = 4 * (e >> 6) + (lane >> 4);
       const int cc = min(col, n - 1);
-      double r2 = 0.0;
-#pragma unroll
-      for (int k = 0; k < DM; ++k) {
-        const double t = xr[k] - xs[(size_t)cc * d + min(k, d - 1)];
-        r2 = fma(t, (k < d) ? t : 0.0, r2);
-      }
       double kv;
       if constexpr (GRAD) {
+        double r2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < DM; ++k) {
+          const double t = xr[k] - xs[(size_t)cc * d + min(k, d - 1)];
+          r2 = fma(t, (k < d) ? t : 0.0, r2);
+        }
         kv = os * kernel_dprofile_t<KIND>(r2) * (xg - xs[(size_t)cc * d + gdim]) * ilg;
+      } else if (kx != nullptr) {
+        kv = kx[(size_t)ti * KB * 64 + min(e, KB * 64 - 1)];  // zero outside B x n
       } else {
-        kv = os * kernel_profile_t<KIND>(r2, tab);
+        kv = cross_kernel_term<DM, KIND>(xr, xs + (size_t)cc * d, d, os, tab);
       }
       const double v = (rv && col < n) ? kv : 0.0;
       const double al = als[cc];  // staged only when want_mean; otherwise ignored

@@ -287,8 +287,9 @@ class DiscreteKnowledgeGradient(_Base):
         """KG and dKG/dX for host candidates X (``[*batch, 1, d]`` or ``[B, d]``), as host fp64 tensors of
         shapes ``batch`` and ``X.shape``: what one L-BFGS-B evaluation of ``optimize_acqf`` needs back
         (``bo_loop.py:127-129``, ``batch_limit = 1``).  The same values and gradient as ``forward`` +
-        autograd, with one device round trip: eager launches between one pinned H2D and one pinned D2H
-        copy (``ForwardPlan.forward_grad_host``)."""
+        autograd, with one device round trip and no autograd graph: up to 64 candidate coordinates travel in
+        the first kernel's arguments and the envelope kernel writes [KG | dKG/dX] into pinned host memory
+        (``ForwardPlan.forward_grad_host``; larger batches: one pinned copy each way)."""
         d = self.x_discretisation.shape[-1]
         if X.shape[-1] != d:
             raise RuntimeError(
