@@ -17,7 +17,7 @@ from .errors import BotorchTensorDimensionError, DkgNativeError, NotPSDError, Un
 LIB_PATH = os.environ.get("DKG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native",
                                                      "libdkg.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 DKG_XARG_MAX = 64  # include/dkg.h: largest B * d of dkg_plan_forward_grad_hostx
 DKG_PLAN_GRAD = 1
 DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 6
+#define DKG_ABI_VERSION 7  /* 7: plan flag DKG_PLAN_NO_CHAIN; the plan holds the large-n K(x, X) fill pointers */
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 

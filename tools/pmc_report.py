@@ -2,7 +2,8 @@
 
 usage: python tools/pmc_report.py <outdir> <profiles/tag.json> [profiles/r02/pmc_headline.json]
 
-Per kernel (forward instantiations only): average per launch of every counter,
+Per kernel (forward instantiations only) and per bench.py stage (its kernels summed per forward): average
+per launch of every counter,
 per-wave instruction mix, VALU / MFMA busy fractions and HBM bytes.  Units and
 gfx950 corrections (MI355X_MICROARCH.md "HBM", "Per-instruction cycle constants"):
   * FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE reports half the bytes of a
@@ -16,8 +17,14 @@ import glob
 import json
 import sys
 
-KERNELS = {"cross_root_plan_kernel": "cross_root_kernel", "posterior_cov_kernel": "posterior_cov_kernel",
+KERNELS = {"cross_root_plan_kernel": "cross_root_kernel", "cross_kfill_kernel": "cross_kfill_kernel",
+           "posterior_cov_kernel": "posterior_cov_kernel", "posterior_cov_wide_kernel": "posterior_cov_wide_kernel",
            "envelope_kernel": "envelope_kernel"}
+# bench.py's stages: the kernels one forward launches per stage (large n: the K(x, X) fill before the cross
+# kernel; large B x N: the 64 x 64 covariance blocks), summed per forward
+STAGES = {"cross_root_kernel": ("cross_root_kernel", "cross_kfill_kernel"),
+          "posterior_cov_kernel": ("posterior_cov_kernel", "posterior_cov_wide_kernel"),
+          "envelope_kernel": ("envelope_kernel",)}
 CLOCK_GHZ = 2.4
 SIMDS = 1024
 
@@ -46,6 +53,33 @@ def durations(out):
 def main():
     out, dst = sys.argv[1], sys.argv[2]
     avg, dur = load(out), durations(out)
+    rep = figures(avg, dur)
+    sav, sdur = {}, {}
+    for st, ks in STAGES.items():
+        for k in ks:
+            if k in avg:
+                acc = sav.setdefault(st, {})
+                for c, v in avg[k].items():
+                    acc[c] = acc.get(c, 0.0) + v
+                if k in dur:
+                    sdur[st] = sdur.get(st, 0.0) + dur[k]
+    srep = figures(sav, sdur)
+    for st, ks in STAGES.items():
+        if st in srep:
+            srep[st]["kernels"] = [k for k in ks if k in avg]
+    json.dump({"kernels": rep, "stages": srep}, open(dst, "w"), indent=2)
+    if len(sys.argv) > 3:  # the per-launch figures bench.py reads (roofline traffic / VALU busy), per stage
+        keys = ("hbm_bytes_per_launch", "fetch_bytes_x2", "write_bytes", "valu_busy_simd_cycles",
+                "valu_insts_per_wave", "valu_busy_frac", "mfma_busy_frac", "mfma_f64_tflops_from_mops", "avg_us",
+                "kernels")
+        summ = {n: {k: r[k] for k in keys if k in r} for n, r in srep.items()}
+        summ["_source"] = {"passes": out, "report": dst}
+        json.dump(summ, open(sys.argv[3], "w"), indent=2)
+    print(json.dumps({n: {k: v for k, v in r.items() if k != "counters_per_launch"} for n, r in rep.items()},
+                     indent=1))
+
+
+def figures(avg, dur):
     rep = {}
     for name, c in avg.items():
         w = c.get("SQ_WAVES", 0.0) or 1.0
@@ -71,15 +105,7 @@ def main():
                 # MOPS counts 512-flop units per the gfx94x convention (16x16x4 f64 = 2 MOPS)
                 r["mfma_f64_tflops_from_mops"] = c["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512 / (dur[name] * 1e-6) / 1e12
         rep[name] = r
-    json.dump(rep, open(dst, "w"), indent=2)
-    if len(sys.argv) > 3:  # the per-launch figures bench.py reads (roofline traffic / VALU busy)
-        keys = ("hbm_bytes_per_launch", "fetch_bytes_x2", "write_bytes", "valu_busy_simd_cycles",
-                "valu_insts_per_wave", "valu_busy_frac", "mfma_busy_frac", "mfma_f64_tflops_from_mops", "avg_us")
-        summ = {n: {k: r[k] for k in keys if k in r} for n, r in rep.items()}
-        summ["_source"] = {"passes": out, "report": dst}
-        json.dump(summ, open(sys.argv[3], "w"), indent=2)
-    print(json.dumps({n: {k: v for k, v in r.items() if k != "counters_per_launch"} for n, r in rep.items()},
-                     indent=1))
+    return rep
 
 
 if __name__ == "__main__":
