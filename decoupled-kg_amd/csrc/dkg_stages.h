@@ -249,7 +249,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
           r2 = fma(t, (k < d) ? t : 0.0, r2);
         }
         kv = os * kernel_dprofile_t<KIND>(r2) * (xg - xs[(size_t)cc * d + gdim]) * ilg;
-      } else if (kx != nullptr) {
+      } else if constexpr (KIND < 0) {
         kv = kx[(size_t)ti * KB * 64 + min(e, KB * 64 - 1)];  // zero outside B x n
       } else {
         kv = cross_kernel_term<DM, KIND>(xr, xs + (size_t)cc * d, d, os, tab);
@@ -260,11 +260,15 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
       if (e < fill) kb_lds[e] = (ET)v;
     }
   };
-  switch (o.kernel) {
-    case DKG_MATERN12: fill_loop(std::integral_constant<int, DKG_MATERN12>{}); break;
-    case DKG_MATERN32: fill_loop(std::integral_constant<int, DKG_MATERN32>{}); break;
-    case DKG_RBF: fill_loop(std::integral_constant<int, DKG_RBF>{}); break;
-    default: fill_loop(std::integral_constant<int, DKG_MATERN52>{}); break;
+  if (!GRAD && kx != nullptr) {
+    fill_loop(std::integral_constant<int, -1>{});  // K(x, X) from cross_kfill_kernel
+  } else {
+    switch (o.kernel) {
+      case DKG_MATERN12: fill_loop(std::integral_constant<int, DKG_MATERN12>{}); break;
+      case DKG_MATERN32: fill_loop(std::integral_constant<int, DKG_MATERN32>{}); break;
+      case DKG_RBF: fill_loop(std::integral_constant<int, DKG_RBF>{}); break;
+      default: fill_loop(std::integral_constant<int, DKG_MATERN52>{}); break;
+    }
   }
   // mean partials: lanes l, l^16, l^32, l^48 share a row.
   if (want_mean) {
