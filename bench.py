@@ -585,12 +585,17 @@ def main():
         ws, ms, Ds, _, _, _, tps = setup("stress")
         es = tps.run(1, args.stress_steps, 2, False, world)
         fb = stage_model(ws, ws.m, [mm.num_train for mm in ms.models], Ds.shape[0], ws.B, ws.S, ws.d)
-        st_s = stage_rooflines(tps.plan, tps.Xd, fb, 3, "fp64", {})
+        # the stress workload's own PMC file (profiles/r03/pmc_stress.json) for its stages' traffic / busy figures
+        pmc_s_path = os.path.join(PMC_DIR, "pmc_stress.json")
+        pmc_s = json.load(open(pmc_s_path)) if os.path.exists(pmc_s_path) else {}
+        st_s = stage_rooflines(tps.plan, tps.Xd, fb, 3, "fp64", pmc_s)
         stress = {"workload": "stress", "value": world * ws.B * args.stress_steps / es, "unit": "KG-evals/s",
                   "steps": args.stress_steps, "ms_per_step": es / args.stress_steps * 1e3, "dtype": "f64",
                   "config": {"m": ws.m, "n_train": ws.n_train, "n_disc": Ds.shape[0], "S": ws.S, "B": ws.B,
                              "d": ws.d},
-                  "stages": {k: {kk: v[kk] for kk in ("avg_launch_us", "achieved", "frac")} for k, v in st_s.items()}}
+                  "stages": {k: {kk: v[kk] for kk in ("avg_launch_us", "achieved", "frac", "traffic", "valu_busy_frac",
+                                                      "mfma_busy_frac_pmc")} for k, v in st_s.items()},
+                  "pmc_source": os.path.relpath(pmc_s_path, REPO) if pmc_s else None}
         del tps
 
     out = None
