@@ -226,11 +226,9 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->debug_cov = dcov ? std::atoi(dcov) : 0;
   static const char* dst = std::getenv("DKG_DEBUG_STAMPS");
   P->debug_stamp = dst ? std::atoi(dst) : 0;
-  // the fused one-launch forward (dkg_fused.h) on request (DKG_PLAN_FUSED, or DKG_FUSED=1 in the
-  // environment for A/B runs): fp64, staged lines, no test hooks
-  static const char* fused_env = std::getenv("DKG_FUSED");
-  const bool split_stages = !((flags & DKG_PLAN_FUSED) || (fused_env && std::atoi(fused_env))) ||
-                            (flags & DKG_PLAN_FORCE_WALK);
+  // the fused one-launch forward (dkg_fused.h) only on explicit request (DKG_PLAN_FUSED): fp64, staged
+  // lines, no test hooks; its bounded in-launch waits report give-ups through dkg_plan_status
+  const bool split_stages = !(flags & DKG_PLAN_FUSED) || (flags & DKG_PLAN_FORCE_WALK);
   P->sync = reinterpret_cast<unsigned long long*>(ws);
   P->sync_bytes = L.sync_bytes;
   {

@@ -64,8 +64,13 @@ forward_fused_kernel(FusedArgs a) {
     const int grp = id % a.cgroups, oi = (id / a.cgroups) % m, ti = id / (a.cgroups * m);
     unsigned long long* st = kst_slot_wg(a.dst, P, 0, id);
     KST_BEGIN(st);
-    if (id == 0) {  // the KG accumulators and arrival tickets the envelope stage adds into (write-through)
-      for (int i = threadIdx.x; i < a.B; i += blockDim.x) {
+    if (grp == 0 && oi == 0) {
+      // the KG accumulators and arrival tickets of this row tile's candidates, which the envelope stage adds
+      // into (write-through): zeroed inside the dependency chain (this workgroup's cnt1 arrival -> the
+      // covariance workgroups of output 0 in this row block -> cnt2 -> the envelope's wait), so every
+      // zero store is visible before any envelope workgroup of these candidates adds to it
+      const int r1 = std::min(a.B, 16 * (ti + 1));
+      for (int i = 16 * ti + (int)threadIdx.x; i < r1; i += blockDim.x) {
         st_out<true>(&a.kg[i], 0.0);
         st_out<true>(&P->tickets[i], 0);
       }

@@ -11,6 +11,7 @@ from .discretekg import (
     calculate_epigraph_indices_batched,
     calculate_expected_value_of_piecewise_linear_function,
     calculate_discrete_kg_conditioning_on_single_output,
+    clear_state_cache,
     kg_from_lines,
     t_batch_mode_transform,
 )
@@ -26,6 +27,7 @@ __all__ = [
     "calculate_epigraph_indices_batched",
     "calculate_expected_value_of_piecewise_linear_function",
     "calculate_discrete_kg_conditioning_on_single_output",
+    "clear_state_cache",
     "kg_from_lines",
     "t_batch_mode_transform",
     "BotorchTensorDimensionError",

@@ -73,16 +73,24 @@ def _as_model_state(model) -> ModelListGPState:
     return from_botorch(model)
 
 
+_BY_VALUE_NUMEL = 64  # tensors this small are fingerprinted by value as well
+
+
 def _fingerprint(obj):
     """What the fitted state of ``model`` is made of, cheaply: every tensor by (identity, in-place
     version counter), every other field by value.  The reference reads the model live at every
     forward (``model.posterior``, discretekg.py:182-185, 275-284); the device state is rebuilt
     whenever this changes (a refit, new training data, an in-place edit)."""
     if isinstance(obj, torch.Tensor):
+        if obj.numel() <= _BY_VALUE_NUMEL and obj.device.type == "cpu":
+            # hyperparameters (lengthscales, outputscale, noise, constant mean, Standardize buffers): by value,
+            # since gpytorch's initialize() and constraint setters write them through .data, which does not
+            # bump the version counter
+            return (id(obj), obj._version, tuple(obj.detach().reshape(-1).tolist()))
         return (id(obj), obj._version)
     if isinstance(obj, ModelListGPState):  # flat, no recursion: this runs on every forward
-        return tuple((id(m.train_x), m.train_x._version, id(m.train_y), m.train_y._version, id(m.lengthscale),
-                      m.lengthscale._version, m.outputscale, m.noise, m.mean_constant, m.kernel, m.nu, m.y_mean,
+        return tuple((id(m.train_x), m.train_x._version, id(m.train_y), m.train_y._version,
+                      _fingerprint(m.lengthscale), m.outputscale, m.noise, m.mean_constant, m.kernel, m.nu, m.y_mean,
                       m.y_std) for m in obj.models)
     if isinstance(obj, SingleTaskGPState):
         return _fingerprint(ModelListGPState(obj))
@@ -104,6 +112,12 @@ def _fingerprint(obj):
 # holds its model's tensors alive, so no live tensor can take over an id in its fingerprint.
 _STATE_CACHE: list = []
 _STATE_CACHE_SIZE = 4
+
+
+def clear_state_cache() -> None:
+    """Drop every shared device state (e.g. between BO iterations, after a refit): the next acquisition
+    rebuilds its caches, and the device memory of the dropped states is released with their last user."""
+    _STATE_CACHE.clear()
 
 
 def shared_state(state: ModelListGPState, fp, x_discretisation: Tensor, device, owner=None) -> DeviceGPState:

@@ -207,6 +207,14 @@ class ForwardPlan:
                                                current_stream_ptr(self.device)), "dkg_plan_status")
         return err.value
 
+    def _check_handoffs(self) -> None:
+        """A fused launch whose bounded in-launch waits gave up computed on unready data: raise on the call
+        that produced it (and reset the bits, so the next call starts clean)."""
+        bits = self.status(reset=True)
+        if bits:
+            raise RuntimeError(f"fused Discrete-KG forward: in-launch hand-off wait gave up (bits 0x{bits:x}); "
+                               "the result is invalid")
+
     def forward_into(self, X: torch.Tensor, kg: torch.Tensor, kg_pairs=None) -> None:
         """Hot path: X (device, B x d, contiguous fp64) -> kg (device, B)."""
         st = self._fwd(self.host, self._dev_ptr, X.data_ptr(), X.shape[0], kg.data_ptr(),
@@ -228,6 +236,8 @@ class ForwardPlan:
         self.forward_into(X, kg, pairs)
         _lib.check(_lib.load().dkg_plan_hull_sizes(self.host, _lib.ptr(hull), B, current_stream_ptr(self.device)),
                    "dkg_plan_hull_sizes")
+        if self.fused:
+            self._check_handoffs()
         return kg, pairs, hull
 
     def lines(self, X: torch.Tensor):
@@ -375,6 +385,8 @@ class ForwardPlan:
             out.copy_(kg, non_blocking=True)
             self._done.record(stream)
             self._done.synchronize()
+            if self.fused:
+                self._check_handoffs()
             return out.clone()
 
     def time_stage(self, X: torch.Tensor, stage: int, reps: int) -> float:

@@ -29,3 +29,27 @@ def test_fingerprint_tracks_refits_and_in_place_edits():
     assert fp2 != fp
     m.models[0].noise = 1e-3
     assert _fingerprint(m) != fp2
+
+
+def test_fingerprint_sees_hyperparameters_written_through_data():
+    """gpytorch's initialize() / constraint setters write hyperparameters through .data (no version bump):
+    small tensors are fingerprinted by value too, so the shared device state is not reused stale."""
+    x = torch.rand(10, 2, dtype=torch.double)
+    m = ModelListGPState(SingleTaskGPState(x, torch.rand(10, dtype=torch.double), [0.2, 0.3], 1.0, 1e-4))
+    fp = _fingerprint(m)
+    m.models[0].lengthscale.data.copy_(torch.tensor([0.25, 0.3], dtype=torch.double))
+    assert _fingerprint(m) != fp
+    mod = torch.nn.Module()
+    mod.raw = torch.nn.Parameter(torch.zeros(3, dtype=torch.double))
+    f1 = _fingerprint(mod)
+    mod.raw.data.copy_(torch.ones(3, dtype=torch.double))
+    assert _fingerprint(mod) != f1
+
+
+def test_clear_state_cache():
+    from dkg_amd import clear_state_cache
+    from dkg_amd.discretekg import _STATE_CACHE
+
+    _STATE_CACHE.append(("fp", None, None, None, None))
+    clear_state_cache()
+    assert _STATE_CACHE == []

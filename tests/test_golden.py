@@ -9,11 +9,14 @@ GPU: the HIP path through the C ABI matches them within the stated tolerance
 import pytest
 import torch
 
-from helpers import LINE_RTOL, assert_within, check_parity_case, load_golden, parity_case, stated_tol
+from helpers import assert_within, check_parity_case, load_golden, parity_case, stated_tol
 from oracle.discretekg import (calculate_discrete_kg, calculate_discrete_kg_conditioning_on_single_output,
                                discrete_kg_batched, kg_pairs_from_lines, lines_batched)
 
 NAMES = ["lengthscales0", "observationnoise0"]
+# the oracle's own lines against the committed ones (CPU): the host-BLAS summation-order gap, not the
+# device-vs-oracle LINE_RTOL
+GOLDEN_LINE_RTOL = 1e-10
 PATHS = [("full", None), ("t0", 0), ("t1", 1)]
 
 
@@ -29,12 +32,12 @@ def test_oracle_reproduces_golden(name):
     assert_within(got_full, t["kg_full"][idx], stated_tol(t["kg_full"][idx], amax_full))
     assert_within(got_t1, t["kg_t1"][idx], stated_tol(t["kg_t1"][idx], amax_t1))
     # the lines themselves: a BLAS summing in another order, through the conditioning of K(D, D),
-    # moves them by ~1e-12 of the largest line (6e-12 at max|a| = 10 on the MI355X box's host):
-    # LINE_RTOL of it, the bound the device lines are held to
+    # moves them by ~1e-13 of the largest line (6e-12 at max|a| = 10 on the MI355X box's host, 0 in the
+    # build container): GOLDEN_LINE_RTOL, a little above that gap, so drift in the restatement shows
     a, b = lines_batched(om, X[:4], D, W, None)
     for got, ref in ((a, t["lines_a"]), (b, t["lines_b"])):
         scale = ref.abs().amax((-1, -2), keepdim=True)
-        assert_within(got, ref, (LINE_RTOL * scale).expand_as(ref), what="line")
+        assert_within(got, ref, (GOLDEN_LINE_RTOL * scale).expand_as(ref), what="line")
 
 
 @pytest.mark.parametrize("name", NAMES)

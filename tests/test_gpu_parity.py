@@ -213,7 +213,7 @@ def test_forward_vs_faithful_oracle(workload, target):
     assert bool((got >= 0).all())
 
 
-@pytest.mark.parametrize("workload,nX", [("small", 32), ("parity6d", 32), ("headline", 128)])
+@pytest.mark.parametrize("workload,nX", [("small", 32), ("parity6d", 32), ("headline", 128), ("headline_nd", 128)])
 @pytest.mark.parametrize("target", [None, 0, 1])
 def test_forward_vs_oracle_all_candidates(workload, nX, target):
     """Every candidate of the workload: lines within LINE_RTOL of the oracle's, the envelope at the
@@ -222,6 +222,9 @@ def test_forward_vs_oracle_all_candidates(workload, nX, target):
 
     model, D, X, W = make_problem(WORKLOADS[workload])
     res = parity_case(model, D, W, X[:nX], target)
+    if workload == "headline_nd":
+        # every pair walks an envelope there (KG > 0 on every candidate): the assertion is not a zero check
+        assert res["kg_zero_frac"] == 0.0
     print(f"{workload} target={target}: " + ", ".join(f"{k}={v:.3g}" for k, v in res.items()
                                                      if not k.startswith("_") and isinstance(v, float)))
     check_parity_case(res)
