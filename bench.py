@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--graph-head", type=int, default=1,
                     help="--graph 2: each stream's period graph split into its first GRAPH_HEAD forwards and the rest, "
                          "the heads of all streams launched first (0 = one graph per stream)")
+    ap.add_argument("--launch-threads", type=int, default=-1,
+                    help="--graph 2: host threads enqueuing the streams' graphs side by side (dkg_launcher; "
+                         "-1 = one per stream, 1 = the caller alone, in stream order)")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")
     ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
     ap.add_argument("--nd-steps", type=int, default=256,
@@ -210,6 +213,7 @@ class Throughput:
         self.main = torch.cuda.current_stream(dev)
         self.f32 = precision == "fp32"
         self.head = 0
+        self.launch_threads = -1
 
     def run(self, ns, steps, warmup, graph, world):
         E, xchg, main_s, dev = self.E, self.xchg, self.main, self.dev
@@ -238,6 +242,7 @@ class Throughput:
         xchg.flush(warmup)
         torch.cuda.synchronize()
         graphs = []
+        launcher = None
         if graph == 2 and steps >= E:
             # per stream one single-stream graph of its rows r = i mod ns: replayed on its own stream, each
             # enqueues its forwards as one batch (a graph forked over streams replays node by node)
@@ -267,6 +272,15 @@ class Throughput:
             execs = [[[ctypes.c_void_p(g.raw_cuda_graph_exec()) for g in pieces] for pieces in gs] for gs in graphs]
             npieces = max(len(p) for gs in graphs for p in gs)
             sptrs = [ctypes.c_void_p(s.cuda_stream) for s in streams]
+            # the streams' graphs enqueued side by side, one host thread per stream (dkg_launcher)
+            nthr = ns if self.launch_threads < 0 else max(1, min(ns, self.launch_threads))
+            if nthr > 1:
+                from dkg_amd.launch import GraphLauncher
+
+                launcher = GraphLauncher(nthr)
+                for slot in range(2):
+                    launcher.prepare(slot, [s.cuda_stream for s in streams],
+                                     [[g.value for g in pieces] for pieces in execs[slot]])
             # the fork / join events, created once (torch's wait_stream creates an event per call)
             evs = [ctypes.c_void_p() for _ in range(ns)]
             for e in evs:
@@ -299,6 +313,8 @@ class Throughput:
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        if graphs and graph == 2 and launcher is not None:
+            launcher.arm(5.0 + 1e-4 * steps)  # workers spin through the timed region
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record()
@@ -319,10 +335,13 @@ class Throughput:
                         hip_check(hip.hipEventRecord(evs[0], sptrs[0]), "hipEventRecord")
                         for i in range(1, ns):
                             hip_check(hip.hipStreamWaitEvent(sptrs[i], evs[0], 0), "hipStreamWaitEvent")
-                    for p in range(npieces):
-                        for i, pieces in enumerate(execs[(k0 // E) % 2]):
-                            if p < len(pieces):
-                                hip_check(hip.hipGraphLaunch(pieces[p], sptrs[i]), "hipGraphLaunch")
+                    if launcher is not None:
+                        launcher.launch((k0 // E) % 2)
+                    else:
+                        for p in range(npieces):
+                            for i, pieces in enumerate(execs[(k0 // E) % 2]):
+                                if p < len(pieces):
+                                    hip_check(hip.hipGraphLaunch(pieces[p], sptrs[i]), "hipGraphLaunch")
                     for i in range(1, ns):
                         hip_check(hip.hipEventRecord(evs[i], sptrs[i]), "hipEventRecord")
                         hip_check(hip.hipStreamWaitEvent(sptrs[0], evs[i], 0), "hipStreamWaitEvent")
@@ -343,6 +362,9 @@ class Throughput:
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         self.host_us_per_step = host / max(1, steps) * 1e6
+        if graphs and graph == 2 and launcher is not None:
+            launcher.arm(0.0)
+            launcher.close()
         # this rank's device time of the forwards, and what the last exchange adds after them (exposed)
         self.compute_ms = ev0.elapsed_time(evc)
         self.exposed_ms = evc.elapsed_time(ev1)
@@ -433,15 +455,19 @@ def main():
                 X = torch.quasirandom.SobolEngine(w.d, scramble=True, seed=4 + 1000 * rank).draw(w.B, dtype=torch.double)
             W_local = W
         else:
-            # weak scaling: S rows per rank out of S*world (rank 0's rows are the workload's W)
-            W_all = W if world == 1 else torch.cat([W, sample_simplex(w.m, w.S * (world - 1), qmc=True, seed=99)])
-            W_local = W_all[rank * w.S:(rank + 1) * w.S]
+            # weak scaling: S rows per rank out of S*world rows of one qMC simplex sample, dealt round robin
+            # (rank r takes rows r, r + world, ...), so every rank's rows spread over the simplex alike and
+            # the ranks' flat / walked pair mixes match statistically (per_rank.batch_stats shows them); at
+            # world = 1 this is the workload's W itself (the same sample_simplex draw)
+            W_all = W if world == 1 else sample_simplex(w.m, w.S * world, qmc=True, seed=11, dtype=torch.double)
+            W_local = W_all[rank::world].contiguous()
         acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev,
                                         precision=args.precision)
         E = max(1, min(args.exchange_every, args.steps))
         tp = Throughput(acq, X, w.B, E, "gather" if args.shard == "candidates" else "reduce", w.S, dev,
                         args.precision)
         tp.head = args.graph_head
+        tp.launch_threads = args.launch_threads
         return w, model, D, X0, W, acq, tp
 
     w, model, D, X0, W, acq, tp = setup(args.workload)
@@ -460,7 +486,8 @@ def main():
     per_rank = {"compute_ms": [float(r[0]) for r in allr], "exposed_collective_ms": [float(r[1]) for r in allr],
                 "elapsed_ms": [float(r[2]) for r in allr],
                 "what": "compute: HIP events from the start of the timed region to the last forward enqueued; "
-                        "exposed: from there to the end of the final exchange (the collective nothing overlaps)"}
+                        "exposed: from there to the end of the final exchange (the collective nothing overlaps); "
+                        "batch_stats: each rank's own pairs (its weight rows x its candidates)"}
 
     # ---- per-kernel rooflines; the dominant kernel's is the line's `roofline`
     pmc = {}
@@ -487,6 +514,18 @@ def main():
     fwd_roof = {"definition": "BASELINE.md: max(F/P_fp64, Bytes/BW_HBM) / T_forward", "flops": f_fwd,
                 "bytes": b_fwd, "t_min_us": t_min * 1e6, "t_forward_us": t_fwd * 1e6, "frac": t_min / t_fwd}
     stats = batch_stats(tp.plan, tp.Xd)
+    # every rank's pair mix (the work a weak-scaling rank does depends on how many of its pairs walk an envelope)
+    mine_st = torch.tensor([stats["zero_kg_frac"], stats["short_circuit_frac"], stats["envelope_lines_mean"],
+                            (1.0 - stats["zero_kg_frac"]) * stats["pairs"]], dtype=torch.double, device=dev)
+    if world > 1:
+        all_st = [torch.zeros_like(mine_st) for _ in range(world)]
+        dist.all_gather(all_st, mine_st)
+    else:
+        all_st = [mine_st]
+    per_rank["batch_stats"] = {"zero_kg_frac": [float(r[0]) for r in all_st],
+                               "short_circuit_frac": [float(r[1]) for r in all_st],
+                               "envelope_lines_mean": [float(r[2]) for r in all_st],
+                               "pairs_with_kg_above_0": [int(round(float(r[3]))) for r in all_st]}
 
     # ---- value + gradient (dkg_plan_forward_grad: the optimize_acqf L-BFGS-B path), same batch
     grad_info = None
@@ -629,7 +668,9 @@ def main():
                        "hip_graph": {0: "off", 1: "one graph forked over the streams",
                                      2: "one single-stream graph per stream"}.get(args.graph, str(args.graph))
                        + (f" (first {args.graph_head} forward(s) of every stream launched first)"
-                          if args.graph == 2 and args.graph_head > 0 else "")},
+                          if args.graph == 2 and args.graph_head > 0 else "")
+                       + (f", enqueued by {max(1, args.streams) if args.launch_threads < 0 else args.launch_threads}"
+                          " host thread(s) side by side (dkg_launcher)" if args.graph == 2 else "")},
             "host_launch_us_per_step": tp.host_us_per_step,
             "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,

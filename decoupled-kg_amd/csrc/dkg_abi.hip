@@ -26,6 +26,16 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+}  // namespace
+
+// dkg_kernels.h: the thread-local error message of the other host translation units (dkg_launch.hip)
+int dkg::report_error(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+
+namespace {
+
 int hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) return fail(DKG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
   return DKG_OK;
@@ -111,11 +121,13 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
     L.var[i] = L.var_all + (size_t)i * Bp * sizeof(double);
   }
   int sw, split;
-  envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split);
+  envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split, !(flags & DKG_PLAN_FUSED));
+  // split > 1: every pair's KG (and, value+gradient, its dKG/dx) for the last workgroup's ordered sums
   L.wg_part = off;
-  off = align256(off + (size_t)std::max(B, 1) * split * sizeof(double));
-  L.wg_gpart = off;  // value+gradient with split > 2: the gradient's per-workgroup partials, summed in order
-  off = align256(off + ((flags & DKG_PLAN_GRAD) && split > 2 ? (size_t)std::max(B, 1) * split * d * sizeof(double) : 0));
+  off = align256(off + (split > 1 ? (size_t)std::max(B, 1) * std::max(S, 1) * sizeof(double) : 0));
+  L.wg_gpart = off;
+  off = align256(off + ((flags & DKG_PLAN_GRAD) && split > 1 ? (size_t)std::max(B, 1) * std::max(S, 1) * d * sizeof(double)
+                                                             : 0));
   L.tickets = off;
   off = align256(off + Bp * sizeof(int));
   L.hull_pairs = off;
@@ -150,7 +162,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   if (target < -1 || target >= m) return fail(DKG_ERR_ARG, "target_output_ix=%d out of range for %d outputs", target, m);
   if (N > (1 << 22)) return fail(DKG_ERR_UNSUPPORTED, "N=%d discretisation points (supported <= %d)", N, 1 << 22);
   int sw, split;
-  envelope_geometry(std::max(max_B, 1), S, &sw, &split);
+  envelope_geometry(std::max(max_B, 1), S, &sw, &split, !(flags & DKG_PLAN_FUSED));
   int max_np = 16;
   for (int i = 0; i < m; ++i) max_np = std::max(max_np, pad16(outs[i].n));
   // the envelope stages the line data in LDS when it fits and the lines fit
@@ -361,8 +373,8 @@ static int* prepare_info(void* work, int n) {
 
 // psd_safe_cholesky's attempts first .. max_tries of one output (attempt 0: no jitter; then absolute jitter
 // 1e-8 * 10^(attempt - 1)), each checked on the host.  *jit: the jitter that worked.
-static int cholesky_attempts(const dkg_output* o, int d, double* L, int* info, int first, int max_tries, hipStream_t s,
-                             double* jit) {
+static int cholesky_attempts(const dkg_output* o, int d, double* L, double* X, int* info, int first, int max_tries,
+                             hipStream_t s, double* jit) {
   int st, h_info = 1;
   for (int attempt = first; attempt <= max_tries; ++attempt) {
     *jit = attempt == 0 ? 0.0 : 1e-8 * std::pow(10.0, attempt - 1);
@@ -370,7 +382,7 @@ static int cholesky_attempts(const dkg_output* o, int d, double* L, int* info, i
                         "kernel_matrix")))
       return st;
     if ((st = hip_check(hipMemsetAsync(info, 0, sizeof(int), s), "hipMemsetAsync")) ||
-        (st = hip_check(launch_cholesky(L, o->n, info, s), "cholesky")) ||
+        (st = hip_check(launch_cholesky(L, X, o->n, info, s), "cholesky")) ||
         (st = hip_check(hipMemcpyAsync(&h_info, info, sizeof(int), hipMemcpyDeviceToHost, s), "hipMemcpyAsync")) ||
         (st = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize")))
       return st;
@@ -389,7 +401,7 @@ int dkg_prepare_output(const dkg_output* o, int d, const double* train_y, int ma
   double* X = static_cast<double*>(work);
   int* info = prepare_info(work, n);
   double jit = 0.0;
-  if ((st = cholesky_attempts(o, d, L, info, 0, max_tries, s, &jit))) return st;
+  if ((st = cholesky_attempts(o, d, L, X, info, 0, max_tries, s, &jit))) return st;
   if (jitter_used) *jitter_used = jit;
   if ((st = hip_check(launch_tri_inverse(L, X, n, info, s), "tri_inverse")) ||
       (st = hip_check(launch_alpha(X, train_y, o->mean_constant, n, alpha, info, s), "alpha")) ||
@@ -430,7 +442,8 @@ int dkg_prepare_outputs(const dkg_output* outs, int m, int d, const double* cons
       return st;
   if ((st = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return st;
   for (int i = 0; i < m; ++i)  // the outputs that need jitter are retried on their own, as dkg_prepare_output
-    if (h_info[i] != 0 && (st = cholesky_attempts(&outs[i], d, L[i], b.info[i], 1, max_tries, s, &jit[i])))
+    if (h_info[i] != 0 &&
+        (st = cholesky_attempts(&outs[i], d, L[i], b.X[i], b.info[i], 1, max_tries, s, &jit[i])))
       return st;
   if ((st = hip_check(launch_tri_inverse_batch(b, m, s), "tri_inverse_batch"))) return st;
   for (int i = 0; i < m; ++i) {

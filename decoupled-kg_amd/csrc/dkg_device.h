@@ -2189,33 +2189,38 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
 #ifndef DKG_STG_STAMPS
   if (!GRAD) KST(st, 5);
 #endif
-  __shared__ int s_lastk;  // G > 2: this workgroup arrived last for its candidate (kg's ticket)
+  // The candidate's KG is (sum of its S pair values in pair order) / S, and dKG/dx likewise, whatever the
+  // launch geometry (waves per workgroup, workgroups per candidate; envelope_geometry): one workgroup sums
+  // its pairs itself; with several, every workgroup leaves its pairs' values in the plan's per-pair slots
+  // and the last to arrive (ticket) sums all S in order, so a narrow small-batch launch, the fused launch
+  // and the wide launch give the same bits.  The last workgroup re-zeroes the ticket for the next launch.
+  __shared__ int s_lastk;  // G > 1: this workgroup arrived last for its candidate (kg's ticket)
   if constexpr (GRAD) {
     if (threadIdx.x < d) {
-      double gs = 0.0;
-      for (int w2 = 0; w2 < SW; ++w2) gs += sgw[w2 * 64 + 48 + threadIdx.x];
-      if (G <= 2) {
-        // at most two workgroups per candidate (S <= 16): two addends onto a zeroed cell commute
-        atomicAdd(&dkg[(size_t)b * d + threadIdx.x], gs / (double)S);
+      if (G == 1) {
+        double gs = 0.0;
+        for (int w2 = 0; w2 < SW; ++w2) gs += sgw[w2 * 64 + 48 + threadIdx.x];
+        gs /= (double)S;
+        dkg[(size_t)b * d + threadIdx.x] = gs;
+        if (hout != nullptr) hout[(size_t)B + (size_t)b * d + threadIdx.x] = gs;
       } else {
-        // more: per-workgroup partials, summed in workgroup order by the last to arrive (below)
-        P->wg_gpart[((size_t)b * G + g) * d + threadIdx.x] = gs / (double)S;
+        for (int q = 0; q < j1 - j0; ++q)
+          P->wg_gpart[((size_t)b * S + j0 + q) * d + threadIdx.x] = sgw[q * 64 + 48 + threadIdx.x];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       }
     }
-    if (G > 2) __syncthreads();  // the partials are out before thread 0 takes the ticket
+    if (G > 1) __syncthreads();  // the partials are out before thread 0 takes the ticket
   }
   if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int q = 0; q < j1 - j0; ++q) s += skg[q];
     if (G == 1) {
+      double s = 0.0;
+      for (int q = 0; q < j1 - j0; ++q) s += skg[q];
       kg[b] = s / (double)S;
-    } else if (G == 2) {
-      // two addends onto a zeroed cell: fp addition commutes, so the order
-      // the two workgroups arrive in does not change the bits.
-      atomicAdd(&kg[b], s / (double)S);
+      if constexpr (GRAD) {
+        if (hout != nullptr) hout[b] = kg[b];
+      }
     } else {
-      P->wg_part[(size_t)b * G + g] = s;
+      for (int q = 0; q < j1 - j0; ++q) P->wg_part[(size_t)b * S + j0 + q] = skg[q];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int prev = atomicAdd(&P->tickets[b], 1);
@@ -2224,9 +2229,10 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         double tot = 0.0;
-        for (int q = 0; q < G; ++q)
-          tot += __hip_atomic_load(&P->wg_part[(size_t)b * G + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int q = 0; q < S; ++q)
+          tot += __hip_atomic_load(&P->wg_part[(size_t)b * S + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         kg[b] = tot / (double)S;
+        __hip_atomic_store(&P->tickets[b], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (GRAD) {
           if (hout != nullptr) hout[b] = kg[b];
         }
@@ -2234,47 +2240,17 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     }
   }
   if constexpr (GRAD) {
-    if (G > 2) {
+    if (G > 1) {
       __syncthreads();
-      if (s_lastk && threadIdx.x < d) {  // the last workgroup: the gradient's partials in workgroup order
+      if (s_lastk && threadIdx.x < d) {  // the last workgroup: the gradient's per-pair partials in pair order
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         double tot = 0.0;
-        for (int q = 0; q < G; ++q)
-          tot += __hip_atomic_load(&P->wg_gpart[((size_t)b * G + q) * d + threadIdx.x], __ATOMIC_RELAXED,
+        for (int q = 0; q < S; ++q)
+          tot += __hip_atomic_load(&P->wg_gpart[((size_t)b * S + q) * d + threadIdx.x], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+        tot /= (double)S;
         dkg[(size_t)b * d + threadIdx.x] = tot;
         if (hout != nullptr) hout[(size_t)B + (size_t)b * d + threadIdx.x] = tot;
-      }
-    }
-  }
-  if constexpr (GRAD) {
-    // hout (dkg_plan_forward_grad_hostx): the candidate's KG and dKG/dx straight into the caller's pinned
-    // host buffer [kg (B) | dkg (B x d)], so no copy follows the launch.  One or two workgroups per
-    // candidate: the second to arrive (ticket; the cross stage zeroed it) reads the sums back after an
-    // acquire.  More: the last workgroup writes them with the ordered sums above.
-    if (hout != nullptr && G <= 2) {
-      __shared__ int s_last;
-      __syncthreads();  // every thread's atomics are issued
-      if (threadIdx.x == 0) {
-        int last = 1;
-        if (G == 2) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          last = atomicAdd(&P->tickets[b], 1) == 1;
-          if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        }
-        s_last = last;
-      }
-      __syncthreads();
-      if (s_last) {
-        if (threadIdx.x == 0)
-          hout[b] = __hip_atomic_load(&kg[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (threadIdx.x < d)
-          hout[(size_t)B + (size_t)b * d + threadIdx.x] =
-              __hip_atomic_load(&dkg[(size_t)b * d + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }

@@ -61,9 +61,9 @@ struct Plan {
   double* cov_all;                  // [max_B][N][cov_rec(m)] posterior covariance rows, line records (workspace)
   double* mu_all;                   // [N][cov_rec(m)] the outputs' disc_mean, line records
   int64_t cov_stride;               // N * cov_rec(m): doubles per candidate in cov_all
-  double* wg_part;                  // [B x split] partial sums (split > 2 only)
-  int* tickets;                     // [B] arrival counters (split > 2; value+gradient with a host output: split 2)
-  double* wg_gpart;                 // GRAD: [B x split x d] per-workgroup dKG/dx partials (split > 2 only)
+  double* wg_part;                  // [B x S] per-pair KG for the ordered sum over S (split > 1 only)
+  int* tickets;                     // [B] arrival counters (split > 1; the last workgroup re-zeroes its own)
+  double* wg_gpart;                 // GRAD: [B x S x d] per-pair dKG/dx for the ordered sum (split > 1 only)
   float* q32[DKG_MAX_OUTPUTS];      // F32: quad-packed K(x, X) R per output (workspace)
   float* root32[DKG_MAX_OUTPUTS];   // F32: quad-packed R^T (fp32 copy of root_frag, plan init)
   float* disc32[DKG_MAX_OUTPUTS];   // F32: quad-packed Q_D (fp32 copy of disc_frag, plan init)
@@ -86,11 +86,13 @@ struct CrossArgs {
 hipError_t launch_kernel_matrix(const dkg_output& o, int d, const double* x1, int n1, const double* x2, int n2,
                                 double diag_add, double* out, hipStream_t s);
 hipError_t launch_pack_root(const double* r, int n, double* rf, hipStream_t s);
-// State preparation (dkg_linalg.hip): blocked Cholesky with device status,
-// triangular inverse, alpha = Linv^T Linv (y - c), root_frag from Linv.
-hipError_t launch_cholesky(double* A, int n, int* info, hipStream_t s);
+// State preparation (dkg_linalg.hip): blocked Cholesky with device status (L in A's lower triangle, the
+// inverses of its diagonal blocks in X's), triangular inverse X = L^{-1}, alpha = Linv^T Linv (y - c),
+// root_frag from Linv.
+hipError_t launch_cholesky(double* A, double* X, int n, int* info, hipStream_t s);
 // Several outputs' factorisations side by side: every launch of the blocked chains carries all of them
-// (blockIdx.y / z = output).  A = the matrix (Cholesky) or L (inverse), X = the inverse's output.
+// (blockIdx.y = output).  A = the matrix (Cholesky: L on return) , X = the inverse (diagonal blocks written
+// by the Cholesky, the rest by the inverse).
 struct PrepBatch {
   double* A[DKG_MAX_OUTPUTS];
   double* X[DKG_MAX_OUTPUTS];
@@ -127,6 +129,8 @@ hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew,
 // otherwise the three stage kernels.  Same bits.
 // Dynamic LDS bytes of the fused forward for a plan (dkg_fused.h fused_lds_bytes).
 size_t fused_lds_bytes_host(const Plan& h);
+// Sets dkg_last_error()'s thread-local message (host translation units other than dkg_abi.hip); returns code.
+int report_error(int code, const char* msg);
 hipError_t launch_forward_auto(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg,
                                double* pairs, hipStream_t s);
 // Envelope stage alone over P sets of L lines: KG, envelope sizes (nullable) and, when idx is given, the
@@ -145,7 +149,7 @@ hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStr
 
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and
 // workgroups per candidate.
-void envelope_geometry(int B, int S, int* waves_per_wg, int* split);
+void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow);
 size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad = false);
 size_t cross_root_lds_bytes(int np, int d);
 

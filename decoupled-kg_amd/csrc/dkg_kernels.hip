@@ -393,12 +393,18 @@ static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const doubl
                : launch_cross_cov_tt<DM, double>(h, dev, xnew, B, kg, s, stage);
 }
 
-void envelope_geometry(int B, int S, int* waves_per_wg, int* split) {
+void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow) {
   // Up to 8 scalarisation waves of one candidate per workgroup, one pair per
   // wave; with S <= 16 at most two workgroups per candidate, whose partial
   // sums meet in one commutative atomic add (no inter-workgroup fences).
-  (void)B;
-  const int sw = std::max(1, std::min(8, S));
+  // Small batches (narrow): fewer waves per workgroup until the launch has at least ENV_MIN_WGS
+  // workgroups, so a B = 1 value+gradient call (the reference's optimize_acqf shape, batch_limit 1)
+  // spreads its S pairs over S CUs, one wave per SIMD, instead of two workgroups; more than two
+  // workgroups per candidate meet in the ordered per-workgroup partials (deterministic).
+  constexpr int ENV_MIN_WGS = 128;
+  int sw = std::max(1, std::min(8, S));
+  if (narrow)
+    while (sw > 1 && (long long)B * ((S + sw - 1) / sw) < ENV_MIN_WGS) sw = (sw + 1) / 2;
   *waves_per_wg = sw;
   *split = (S + sw - 1) / sw;
 }

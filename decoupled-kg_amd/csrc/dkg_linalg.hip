@@ -17,25 +17,32 @@ namespace dkg {
 
 constexpr int LB = 32;  // block width
 
+// Lower tile (ti, tj), tj <= ti, of the row-major enumeration t = ti (ti + 1) / 2 + tj.
+__device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
+  ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  while (ti * (ti + 1) / 2 > t) --ti;
+  tj = t - ti * (ti + 1) / 2;
+}
+
 // ---------------------------------------------------------------------------
-// Cholesky panel at block column k0: factor A[k0:k0+nb, k0:k0+nb] in LDS and
-// solve the rows below it, A[i, k0:k0+nb] <- A[i, k0:k0+nb] Lkk^{-T}.
-// info (device): 0 = fine; j + 1 = the pivot of column j is not positive/finite
-// (LAPACK potrf convention, what cholesky_ex reports).
-__device__ __forceinline__ void chol_panel_body(double* __restrict__ A, int n, int k0, int* __restrict__ info) {
-  __shared__ double Lk[LB][LB + 1];
+// The diagonal block kb of one output, updated and held in LDS (sC, lower triangle valid): factor it
+// (L_kk), invert it (W_kk = L_kk^{-1}), store L_kk into A's lower block (the block's upper part zeroed)
+// and W_kk into X's diagonal block (the final inverse's diagonal block).  info: LAPACK potrf convention
+// (first failing column + 1; NaN and non-positive pivots fail).  Called by the whole workgroup.
+__device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __restrict__ X, int n, int kb,
+                                            int* __restrict__ info, double (*sC)[LB + 1], double (*sL)[LB + 1]) {
   __shared__ int bad;
-  if (*info != 0) return;  // an earlier panel failed: nothing more to do
-  const int nb = min(LB, n - k0);
+  const int k0 = kb * LB, nb = min(LB, n - k0);
   const int tid = threadIdx.x;
   if (tid < 64) {
-    // the diagonal block on one wave, in registers: lane r holds row r (zero rows past nb); column j's
-    // pivot and entries reach the other lanes by v_readlane, so the 32 steps need no LDS round trip
-    // and no barrier (the LDS version spent ~0.7 us per step on three barriers)
+    // one wave, lane r holds row r (rows past nb are identity rows); column j's pivot and entries reach
+    // the other lanes by v_readlane, so the 32 steps need no LDS round trip and no barrier
     const int lane = tid;
     double a[LB];
 #pragma unroll
-    for (int c = 0; c < LB; ++c) a[c] = (lane < nb && c <= lane) ? A[(size_t)(k0 + lane) * n + k0 + c] : 0.0;
+    for (int c = 0; c < LB; ++c)
+      a[c] = (lane < nb) ? ((c <= lane) ? sC[lane][c] : 0.0) : ((c == lane) ? 1.0 : 0.0);
     int fail = 0;
 #pragma unroll
     for (int j = 0; j < LB; ++j) {
@@ -58,7 +65,7 @@ __device__ __forceinline__ void chol_panel_body(double* __restrict__ A, int n, i
     }
     if (lane < LB) {
 #pragma unroll
-      for (int c = 0; c < LB; ++c) Lk[lane][c] = a[c];
+      for (int c = 0; c < LB; ++c) sL[lane][c] = (c <= lane) ? a[c] : 0.0;
     }
     if (lane == 0) bad = fail;
   }
@@ -67,194 +74,228 @@ __device__ __forceinline__ void chol_panel_body(double* __restrict__ A, int n, i
     if (tid == 0) *info = bad;
     return;
   }
+  if (tid < LB) {
+    // W = L^{-1} by columns: thread c solves L w = e_c (forward substitution; the row of L it needs is the
+    // same for every thread: LDS broadcast reads)
+    const int c = tid;
+    double w[LB];
+#pragma unroll
+    for (int r = 0; r < LB; ++r) {
+      double acc = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = 0; q < r; ++q) acc = fma(-sL[r][q], w[q], acc);
+      w[r] = acc / sL[r][r];
+      asm volatile("" ::: "memory");  // one row of L live at a time (as in the row solves)
+    }
+    if (c < nb) {
+#pragma unroll
+      for (int r = 0; r < LB; ++r)
+        if (r < nb) X[(size_t)(k0 + r) * n + k0 + c] = w[r];
+    }
+  }
   for (int e = tid; e < nb * nb; e += blockDim.x) {
     const int r = e / nb, c = e % nb;
-    if (c <= r) A[(size_t)(k0 + r) * n + k0 + c] = Lk[r][c];
+    A[(size_t)(k0 + r) * n + k0 + c] = sL[r][c];  // zeros above the diagonal
   }
-  // rows below: x Lkk^T = a  (forward substitution over the nb columns)
-  for (int i = k0 + nb + tid; i < n; i += blockDim.x) {
-    double x[LB];
-    double* row = A + (size_t)i * n + k0;
-#pragma unroll
-    for (int c = 0; c < LB; ++c) x[c] = (c < nb) ? row[c] : 0.0;
-#pragma unroll
-    for (int c = 0; c < LB; ++c) {
-      if (c < nb) {
-        double s = x[c];
-#pragma unroll
-        for (int q = 0; q < c; ++q) s -= x[q] * Lk[c][q];
-        x[c] = s / Lk[c][c];
-      }
-      // no LDS read of a later row is hoisted above this one: the unrolled solve would otherwise keep
-      // all 528 Lk values live at once (256 VGPRs and ~700 bytes of scratch per lane)
-      asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int c = 0; c < LB; ++c)
-      if (c < nb) row[c] = x[c];
-  }
-}
-
-__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int n, int k0, int* __restrict__ info) {
-  chol_panel_body(A, n, k0, info);
-}
-
-// All outputs' panels at block column k0 in one launch (blockIdx.y = output; outputs with n <= k0 are done).
-__global__ __launch_bounds__(256) void chol_panel_batch_kernel(PrepBatch b, int k0) {
-  const int i = blockIdx.y;
-  if (k0 < b.n[i]) chol_panel_body(b.A[i], b.n[i], k0, b.info[i]);
-}
-
-// 32 x 32 tile update C -= P Q^T with P = A[pi.., kc..kc+32), Q = A[qi.., kc..kc+32)
-// (row-major, leading dimension n), rows beyond n skipped.  Four waves, one
-// 16 x 16 sub-tile each, eight MFMAs (K = 32).
-__device__ __forceinline__ void tile_update(double* __restrict__ A, const double* __restrict__ Pm,
-                                            const double* __restrict__ Qm, int n, int ci, int cj, int pi, int qi,
-                                            int kc, int kn) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int si = wave >> 1, sj = wave & 1;  // sub-tile
-  const int ra = pi + 16 * si + (lane & 15);  // A operand row (P)
-  const int rb = qi + 16 * sj + (lane & 15);  // B operand column (row of Q)
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int kb = 0; kb < LB / 4; ++kb) {
-    const int kk = 4 * kb + (lane >> 4);
-    const double a = (ra < n && kk < kn) ? Pm[(size_t)ra * n + kc + kk] : 0.0;
-    const double b = (rb < n && kk < kn) ? Qm[(size_t)rb * n + kc + kk] : 0.0;
-    acc = mfma_f64(a, b, acc);
-  }
-  // D lane map: row (l >> 4) + 4 r, column l & 15
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = ci + 16 * si + (lane >> 4) + 4 * r;
-    const int col = cj + 16 * sj + (lane & 15);
-    if (row < n && col < n) A[(size_t)row * n + col] -= acc[r];
-  }
-}
-
-// Trailing update after panel k0: A[i][j] -= sum_c L[i][c] L[j][c] over the
-// panel's columns, for the lower tiles (ti >= tj) of the trailing matrix.
-__device__ __forceinline__ void chol_update_body(double* __restrict__ A, int n, int k0, const int* __restrict__ info,
-                                                 int t) {
-  if (*info != 0) return;
-  const int base = k0 + LB;
-  // t enumerates lower tiles (ti, tj), tj <= ti, row-major over ti
-  int ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-  while (ti * (ti + 1) / 2 > t) --ti;
-  const int tj = t - ti * (ti + 1) / 2;
-  const int ci = base + LB * ti, cj = base + LB * tj;
-  tile_update(A, A, A, n, ci, cj, ci, cj, k0, min(LB, n - k0));
-}
-
-__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int n, int k0,
-                                                          const int* __restrict__ info) {
-  chol_update_body(A, n, k0, info, blockIdx.x);
-}
-
-__global__ __launch_bounds__(256) void chol_update_batch_kernel(PrepBatch b, int k0) {
-  const int i = blockIdx.y;
-  const int T = (b.n[i] - k0 - LB + LB - 1) / LB;  // trailing tiles per side of output i
-  if (T > 0 && (int)blockIdx.x < T * (T + 1) / 2) chol_update_body(b.A[i], b.n[i], k0, b.info[i], blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
-// Triangular inverse X = L^{-1} (lower), right-looking by block rows of the
-// right-hand side I: at step k0 the block row X_k = Lkk^{-1} B_k (B_k holds
-// I_k minus the updates so far, columns < k0 + nb), then
-// B_i -= L_ik X_k for every later block row i.  X overwrites B in `X`.
-__device__ __forceinline__ void trinv_panel_body(const double* __restrict__ L, double* __restrict__ X, int n, int k0,
-                                                 const int* __restrict__ info) {
-  __shared__ double Lk[LB][LB + 1];
-  if (*info != 0) return;
-  const int nb = min(LB, n - k0);
+// Blocked right-looking Cholesky, one launch per block column kb (kb = -1: factor the first diagonal
+// block), all outputs side by side (blockIdx.y = output).  Workgroup (i, j), i >= j > kb, of launch kb:
+//   P = A_ik W_kk^T, Q = A_jk W_kk^T    (the solved panel tiles L_ik, L_jk: MFMA, K = 32)
+//   A_ij -= P Q^T                       (MFMA, K = 32)
+// The diagonal workgroup (i, i) also stores L_ik^T into A's upper block (kb, i) -- nobody reads the upper
+// triangle during the factorisation, so the unsolved A_ik stays readable for the other workgroups of the
+// launch -- and (i = kb + 1) factors and inverts the freshly updated diagonal block (factor_diag).  The
+// panel solves are thereby spread over the update workgroups (the single-wave panel kernels they replace
+// took ~27 us per block column), and one launch per block column remains.  dkg_chol_finalize_kernel moves
+// the panels to the lower triangle at the end.
+__global__ __launch_bounds__(256) void chol_step_kernel(PrepBatch bt, int kb) {
+  __shared__ double sP[LB][LB + 1], sQ[LB][LB + 1], sW[LB][LB + 1];
+  const int o = blockIdx.y;
+  const int n = bt.n[o];
+  double* __restrict__ A = bt.A[o];
+  double* __restrict__ X = bt.X[o];
+  int* info = bt.info[o];
+  if (n <= 0 || *info != 0) return;  // an earlier step failed: nothing more to do
   const int tid = threadIdx.x;
+  const int nbk = (n + LB - 1) / LB;
+  if (kb < 0) {
+    if (blockIdx.x != 0) return;
+    const int nb = min(LB, n);
+    for (int e = tid; e < LB * LB; e += blockDim.x) {
+      const int r = e / LB, c = e % LB;
+      sP[r][c] = (r < nb && c < nb) ? A[(size_t)r * n + c] : 0.0;
+    }
+    __syncthreads();
+    factor_diag(A, X, n, 0, info, sP, sQ);
+    return;
+  }
+  const int T = nbk - kb - 1;
+  if (T <= 0 || (int)blockIdx.x >= T * (T + 1) / 2) return;
+  int ti, tj;
+  lower_tile(blockIdx.x, ti, tj);
+  const int bi = kb + 1 + ti, bj = kb + 1 + tj;
+  const int k0 = kb * LB, i0 = bi * LB, j0 = bj * LB;
   for (int e = tid; e < LB * LB; e += blockDim.x) {
     const int r = e / LB, c = e % LB;
-    Lk[r][c] = (r < nb && c <= r) ? L[(size_t)(k0 + r) * n + k0 + c] : 0.0;
+    sW[r][c] = (k0 + r < n && k0 + c < n) ? X[(size_t)(k0 + r) * n + k0 + c] : 0.0;
   }
   __syncthreads();
-  // columns 0 .. k0 + nb - 1 of block row k: Lkk x = b (forward substitution)
-  for (int c = tid; c < k0 + nb; c += blockDim.x) {
-    double x[LB];
+  const int lane = tid & 63, wave = tid >> 6;
+  const int si = wave >> 1, sj = wave & 1;  // this wave's 16 x 16 sub-tile
+  // solved panel tile: dst[r][c] = sum_q A[r0 + r][k0 + q] W[c][q]
+  auto panel = [&](int r0, double (*dst)[LB + 1]) {
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int ra = r0 + 16 * si + (lane & 15);
 #pragma unroll
-    for (int r = 0; r < LB; ++r) x[r] = (r < nb) ? X[(size_t)(k0 + r) * n + c] : 0.0;
-#pragma unroll
-    for (int r = 0; r < LB; ++r) {
-      if (r < nb) {
-        double s = x[r];
-#pragma unroll
-        for (int q = 0; q < r; ++q) s -= Lk[r][q] * x[q];
-        x[r] = s / Lk[r][r];
-      }
-      asm volatile("" ::: "memory");  // as in chol_panel_kernel: one row of Lk live at a time
+    for (int q = 0; q < LB / 4; ++q) {
+      const int kk = 4 * q + (lane >> 4);
+      const double a = (ra < n && k0 + kk < n) ? A[(size_t)ra * n + k0 + kk] : 0.0;
+      acc = mfma_f64(a, sW[16 * sj + (lane & 15)][kk], acc);
     }
 #pragma unroll
-    for (int r = 0; r < LB; ++r)
-      if (r < nb) X[(size_t)(k0 + r) * n + c] = x[r];
-  }
-}
-
-__global__ __launch_bounds__(256) void trinv_panel_kernel(const double* __restrict__ L, double* __restrict__ X, int n,
-                                                          int k0, const int* __restrict__ info) {
-  trinv_panel_body(L, X, n, k0, info);
-}
-
-__global__ __launch_bounds__(256) void trinv_panel_batch_kernel(PrepBatch b, int k0) {
-  const int i = blockIdx.y;
-  if (k0 < b.n[i]) trinv_panel_body(b.A[i], b.X[i], b.n[i], k0, b.info[i]);
-}
-
-// B_i[:, 0 : k0 + nb) -= L[i-block, k-block] X_k for block rows i > k; grid
-// (column tiles of the first k0 + nb columns, later block rows).
-__device__ __forceinline__ void trinv_update_body(const double* __restrict__ L, double* __restrict__ X, int n, int k0,
-                                                  const int* __restrict__ info, int bx, int by) {
-  if (*info != 0) return;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int si = wave >> 1, sj = wave & 1;
-  const int nb = min(LB, n - k0);
-  const int ci = k0 + LB * (1 + by);  // output rows
-  const int cj = LB * bx;             // output columns
-  const int ra = ci + 16 * si + (lane & 15);  // row of L (A operand)
-  const int cb = cj + 16 * sj + (lane & 15);  // column of X_k (B operand)
+    for (int r = 0; r < 4; ++r) dst[16 * si + (lane >> 4) + 4 * r][16 * sj + (lane & 15)] = acc[r];
+  };
+  panel(i0, sP);
+  if (bi != bj) panel(j0, sQ);
+  __syncthreads();
+  double(*Q)[LB + 1] = (bi == bj) ? sP : sQ;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int kb = 0; kb < LB / 4; ++kb) {
-    const int kk = 4 * kb + (lane >> 4);
-    const double a = (ra < n && kk < nb) ? L[(size_t)ra * n + k0 + kk] : 0.0;
-    const double b = (cb < n && kk < nb) ? X[(size_t)(k0 + kk) * n + cb] : 0.0;
-    acc = mfma_f64(a, b, acc);
+  for (int q = 0; q < LB / 4; ++q) {
+    const int kk = 4 * q + (lane >> 4);
+    acc = mfma_f64(sP[16 * si + (lane & 15)][kk], Q[16 * sj + (lane & 15)][kk], acc);
   }
+  const bool diag_next = (bi == bj) && (bi == kb + 1);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int row = ci + 16 * si + (lane >> 4) + 4 * r;
-    const int col = cj + 16 * sj + (lane & 15);
-    if (row < n && col < k0 + nb) X[(size_t)row * n + col] -= acc[r];
+    const int row = 16 * si + (lane >> 4) + 4 * r, col = 16 * sj + (lane & 15);
+    const bool in = i0 + row < n && j0 + col < n;
+    const double v = in ? A[(size_t)(i0 + row) * n + j0 + col] - acc[r] : 0.0;
+    if (diag_next) sW[row][col] = v;  // sW is free (read before the barrier above)
+    else if (in) A[(size_t)(i0 + row) * n + j0 + col] = v;
+  }
+  if (bi == bj) {
+    // L_ik^T into the upper block (kb, bi): row k0 + c, column i0 + r (r fastest: coalesced)
+    for (int e = tid; e < LB * LB; e += blockDim.x) {
+      const int c = e / LB, r = e % LB;
+      if (i0 + r < n && k0 + c < n) A[(size_t)(k0 + c) * n + i0 + r] = sP[r][c];
+    }
+  }
+  if (diag_next) {
+    __syncthreads();
+    factor_diag(A, X, n, bi, info, sW, sQ);
   }
 }
 
-__global__ __launch_bounds__(256) void trinv_update_kernel(const double* __restrict__ L, double* __restrict__ X, int n,
-                                                           int k0, const int* __restrict__ info) {
-  trinv_update_body(L, X, n, k0, info, blockIdx.x, blockIdx.y);
+// After the factorisation: every panel block L_ik (i > k), held transposed in A's upper block (k, i),
+// moves to the lower block (i, k), and the upper block is zeroed.  Grid (strictly lower tiles, outputs).
+__global__ __launch_bounds__(256) void chol_finalize_kernel(PrepBatch bt) {
+  __shared__ double sT[LB][LB + 1];
+  const int o = blockIdx.y;
+  const int n = bt.n[o];
+  double* __restrict__ A = bt.A[o];
+  if (n <= 0 || *bt.info[o] != 0) return;
+  const int nbk = (n + LB - 1) / LB;
+  if ((int)blockIdx.x >= nbk * (nbk - 1) / 2) return;
+  int ti, tj;
+  lower_tile(blockIdx.x, ti, tj);  // ti >= tj over nbk - 1 rows: the strictly lower tile (ti + 1, tj)
+  const int i0 = (ti + 1) * LB, k0 = tj * LB;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < LB * LB; e += blockDim.x) {
+    const int r = e / LB, c = e % LB;  // upper block row k0 + r, column i0 + c
+    sT[r][c] = (k0 + r < n && i0 + c < n) ? A[(size_t)(k0 + r) * n + i0 + c] : 0.0;
+  }
+  __syncthreads();
+  for (int e = tid; e < LB * LB; e += blockDim.x) {
+    const int r = e / LB, c = e % LB;
+    if (i0 + r < n && k0 + c < n) {
+      A[(size_t)(i0 + r) * n + k0 + c] = sT[c][r];
+      A[(size_t)(k0 + c) * n + i0 + r] = 0.0;
+    }
+  }
 }
 
-__global__ __launch_bounds__(256) void trinv_update_batch_kernel(PrepBatch b, int k0) {
-  const int i = blockIdx.z;
-  const int n = b.n[i];
-  if (k0 >= n) return;
-  const int rows = (n - k0 - LB + LB - 1) / LB, cols = (k0 + LB + LB - 1) / LB;
-  if ((int)blockIdx.x < cols && (int)blockIdx.y < rows) trinv_update_body(b.A[i], b.X[i], n, k0, b.info[i], blockIdx.x, blockIdx.y);
-}
-
-// X = I (row-major n x n) and the upper triangle of L zeroed.
-__global__ void trinv_init_kernel(double* __restrict__ L, double* __restrict__ X, int n) {
-  const size_t total = (size_t)n * n;
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / n), c = (int)(e % n);
-    X[e] = (r == c) ? 1.0 : 0.0;
-    if (c > r) L[e] = 0.0;
+// ---------------------------------------------------------------------------
+// X = L^{-1} by independent column tiles (16 columns per workgroup; the diagonal blocks X_jj = W_jj are
+// already in place from the factorisation): walking down the block rows of the tile,
+//   X_i = -W_ii sum_{k = j}^{i-1} L_ik X_k
+// (L_ik from the finalised lower triangle; the tile's earlier X_k kept in LDS).  Four waves: wave w takes
+// row half w & 1 and the k blocks of parity w >> 1 (the two parities meet in LDS in a fixed order), then
+// two waves apply -W_ii.  The rows above the diagonal block are zeroed.  Grid (n_pad / 16, outputs),
+// dynamic LDS (blocks + 3) * 32 * 16 doubles.
+__global__ __launch_bounds__(256) void trinv_col_kernel(PrepBatch bt) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int o = blockIdx.y;
+  const int n = bt.n[o];
+  const double* __restrict__ L = bt.A[o];
+  double* __restrict__ X = bt.X[o];
+  if (n <= 0 || *bt.info[o] != 0) return;
+  const int c0 = 16 * blockIdx.x;
+  if (c0 >= n) return;
+  const int nbk = (n + LB - 1) / LB;
+  const int bj = c0 / LB;
+  const int nblk = nbk - bj;
+  double* sX = sm;                               // [nblk][LB][16]
+  double* sY = sX + (size_t)nblk * LB * 16;      // [LB][16]
+  double* red = sY + LB * 16;                    // [LB][16]
+  const int tid = threadIdx.x;
+  for (int e = tid; e < bj * LB * 16; e += blockDim.x) {
+    const int r = e / 16, c = e % 16;
+    if (c0 + c < n) X[(size_t)r * n + c0 + c] = 0.0;
+  }
+  for (int e = tid; e < LB * 16; e += blockDim.x) {
+    const int r = e / 16, c = e % 16;
+    sX[e] = (bj * LB + r < n && c0 + c < n) ? X[(size_t)(bj * LB + r) * n + c0 + c] : 0.0;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  const int si = wave & 1, kp = wave >> 1;
+  for (int bi = bj + 1; bi < nbk; ++bi) {
+    const int i0 = bi * LB;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int ra = i0 + 16 * si + (lane & 15);
+    for (int bk = bj + kp; bk < bi; bk += 2) {
+      const double* sxk = sX + (size_t)(bk - bj) * LB * 16;
+#pragma unroll
+      for (int q = 0; q < LB / 4; ++q) {
+        const int kk = 4 * q + (lane >> 4);
+        const double a = (ra < n && bk * LB + kk < n) ? L[(size_t)ra * n + bk * LB + kk] : 0.0;
+        acc = mfma_f64(a, sxk[kk * 16 + (lane & 15)], acc);
+      }
+    }
+    if (kp == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(16 * si + (lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+    }
+    __syncthreads();
+    if (kp == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int idx = (16 * si + (lane >> 4) + 4 * r) * 16 + (lane & 15);
+        sY[idx] = acc[r] + red[idx];
+      }
+    }
+    __syncthreads();
+    if (wave < 2) {
+      d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+      const int rw = 16 * si + (lane & 15);  // row of W_ii
+#pragma unroll
+      for (int q = 0; q < LB / 4; ++q) {
+        const int kk = 4 * q + (lane >> 4);
+        const double a = (i0 + rw < n && i0 + kk < n) ? X[(size_t)(i0 + rw) * n + i0 + kk] : 0.0;
+        acc2 = mfma_f64(a, sY[kk * 16 + (lane & 15)], acc2);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * si + (lane >> 4) + 4 * r, col = lane & 15;
+        const double v = -acc2[r];
+        sX[(size_t)(bi - bj) * LB * 16 + row * 16 + col] = v;
+        if (i0 + row < n && c0 + col < n) X[(size_t)(i0 + row) * n + c0 + col] = v;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -278,15 +319,24 @@ __global__ __launch_bounds__(1024) void alpha_kernel(const double* __restrict__ 
     if (lane == 0) t[i] = s;
   }
   __syncthreads();
-  // alpha = X^T t, one column q per thread summed over i in ascending order; unrolled so that eight
-  // rows' loads are in flight at once (they do not depend on the running sum)
-  for (int q = threadIdx.x; q < pad16(n); q += blockDim.x) {
+  // alpha = X^T t by groups of 64 columns: wave w sums the rows i = w (mod 16) of its lane's column (its
+  // loads independent of each other, all in flight), then the 16 wave partials meet in LDS in wave order
+  __shared__ double part[16][64];
+  for (int g0 = 0; g0 < pad16(n); g0 += 64) {
+    const int q = g0 + lane;
     double s = 0.0;
     if (q < n) {
-#pragma unroll 8
-      for (int i = q; i < n; ++i) s = fma(X[(size_t)i * n + q], t[i], s);  // coalesced across q
+      const int i1 = q + ((wave - q) % nw + nw) % nw;  // first row >= q with i = wave (mod nw)
+      for (int i = i1; i < n; i += nw) s = fma(X[(size_t)i * n + q], t[i], s);  // coalesced across lanes
     }
-    alpha[q] = s;
+    part[wave][lane] = s;
+    __syncthreads();
+    if (wave == 0 && q < pad16(n)) {
+      double a = 0.0;
+      for (int w2 = 0; w2 < nw; ++w2) a += part[w2][lane];
+      alpha[q] = a;
+    }
+    __syncthreads();
   }
 }
 
@@ -309,51 +359,48 @@ __global__ void pack_linv_kernel(const double* __restrict__ X, int n, double* __
 
 static int grid_for(size_t total) { return (int)std::min<size_t>((total + 255) / 256, 4096); }
 
-hipError_t launch_cholesky(double* A, int n, int* info, hipStream_t s) {
-  for (int k0 = 0; k0 < n; k0 += LB) {
-    hipLaunchKernelGGL(chol_panel_kernel, dim3(1), dim3(256), 0, s, A, n, k0, info);
-    const int T = (n - k0 - LB + LB - 1) / LB;  // trailing tiles per side
-    if (T > 0) hipLaunchKernelGGL(chol_update_kernel, dim3(T * (T + 1) / 2), dim3(256), 0, s, A, n, k0, info);
+// Blocked Cholesky of every output (A lower: L; X diagonal blocks: W_kk = L_kk^{-1}): one launch for the
+// first diagonal block, one per further block column, then the panels moved to the lower triangle.
+hipError_t launch_cholesky_batch(const PrepBatch& b, int m, hipStream_t s) {
+  int nmax = 0;
+  for (int i = 0; i < m; ++i) nmax = std::max(nmax, b.n[i]);
+  const int nbk = (nmax + LB - 1) / LB;
+  hipLaunchKernelGGL(chol_step_kernel, dim3(1, m), dim3(256), 0, s, b, -1);
+  for (int kb = 0; kb + 1 < nbk; ++kb) {
+    const int T = nbk - kb - 1;
+    hipLaunchKernelGGL(chol_step_kernel, dim3(T * (T + 1) / 2, m), dim3(256), 0, s, b, kb);
   }
+  if (nbk > 1) hipLaunchKernelGGL(chol_finalize_kernel, dim3(nbk * (nbk - 1) / 2, m), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_cholesky(double* A, double* X, int n, int* info, hipStream_t s) {
+  PrepBatch b{};
+  b.A[0] = A;
+  b.X[0] = X;
+  b.n[0] = n;
+  b.info[0] = info;
+  return launch_cholesky_batch(b, 1, s);
+}
+
+// X = L^{-1} of every output, after launch_cholesky_batch (one launch: independent 16-column tiles).
+hipError_t launch_tri_inverse_batch(const PrepBatch& b, int m, hipStream_t s) {
+  int nmax = 0;
+  for (int i = 0; i < m; ++i) nmax = std::max(nmax, b.n[i]);
+  const int nbk = (nmax + LB - 1) / LB;
+  const size_t lds = (size_t)(nbk + 2) * LB * 16 * sizeof(double);
+  raise_lds_limit((const void*)trinv_col_kernel, lds);
+  hipLaunchKernelGGL(trinv_col_kernel, dim3((nmax + 15) / 16, m), dim3(256), lds, s, b);
   return hipGetLastError();
 }
 
 hipError_t launch_tri_inverse(double* L, double* X, int n, const int* info, hipStream_t s) {
-  hipLaunchKernelGGL(trinv_init_kernel, dim3(grid_for((size_t)n * n)), dim3(256), 0, s, L, X, n);
-  for (int k0 = 0; k0 < n; k0 += LB) {
-    hipLaunchKernelGGL(trinv_panel_kernel, dim3(1), dim3(256), 0, s, L, X, n, k0, info);
-    const int rows = (n - k0 - LB + LB - 1) / LB;
-    const int cols = (k0 + LB + LB - 1) / LB;
-    if (rows > 0) hipLaunchKernelGGL(trinv_update_kernel, dim3(cols, rows), dim3(256), 0, s, L, X, n, k0, info);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_cholesky_batch(const PrepBatch& b, int m, hipStream_t s) {
-  int nmax = 0;
-  for (int i = 0; i < m; ++i) nmax = std::max(nmax, b.n[i]);
-  for (int k0 = 0; k0 < nmax; k0 += LB) {
-    hipLaunchKernelGGL(chol_panel_batch_kernel, dim3(1, m), dim3(256), 0, s, b, k0);
-    const int T = (nmax - k0 - LB + LB - 1) / LB;
-    if (T > 0) hipLaunchKernelGGL(chol_update_batch_kernel, dim3(T * (T + 1) / 2, m), dim3(256), 0, s, b, k0);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_tri_inverse_batch(const PrepBatch& b, int m, hipStream_t s) {
-  int nmax = 0;
-  for (int i = 0; i < m; ++i) {
-    nmax = std::max(nmax, b.n[i]);
-    hipLaunchKernelGGL(trinv_init_kernel, dim3(grid_for((size_t)b.n[i] * b.n[i])), dim3(256), 0, s, b.A[i], b.X[i],
-                       b.n[i]);
-  }
-  for (int k0 = 0; k0 < nmax; k0 += LB) {
-    hipLaunchKernelGGL(trinv_panel_batch_kernel, dim3(1, m), dim3(256), 0, s, b, k0);
-    const int rows = (nmax - k0 - LB + LB - 1) / LB;
-    const int cols = (k0 + LB + LB - 1) / LB;
-    if (rows > 0) hipLaunchKernelGGL(trinv_update_batch_kernel, dim3(cols, rows, m), dim3(256), 0, s, b, k0);
-  }
-  return hipGetLastError();
+  PrepBatch b{};
+  b.A[0] = L;
+  b.X[0] = X;
+  b.n[0] = n;
+  b.info[0] = const_cast<int*>(info);
+  return launch_tri_inverse_batch(b, 1, s);
 }
 
 hipError_t launch_alpha(const double* X, const double* y, double c, int n, double* alpha, const int* info,

@@ -91,6 +91,10 @@ SIGNATURES = {
     "dkg_epigraph": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dkg_pwl_expectation": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "dkg_plan_lines": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_launcher_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "dkg_launcher_arm": (c_int, [c_void_p, c_double]),
+    "dkg_launcher_graphs": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(c_int), POINTER(c_void_p)]),
+    "dkg_launcher_destroy": (c_int, [c_void_p]),
     "dkg_debug_read_kstamps": (c_int, [c_void_p, c_int]),
     "dkg_debug_wave_ops": (c_int, [c_void_p, c_void_p, c_void_p]),
     "dkg_debug_mfma_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),

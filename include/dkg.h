@@ -304,6 +304,21 @@ int dkg_debug_wave_ops(const double* in, double* out, void* stream);
  * v_mfma_f64_16x16x4_f64 using the operand/result lane maps the kernels assume. */
 int dkg_debug_mfma_f64(const double* a, const double* b, double* c, void* stream);
 
+/* ---- Launcher: captured forward graphs of several streams enqueued side by side from host threads.
+ * A hipGraphLaunch costs ~1 us of host time per kernel node plus ~9 us; one thread launching every
+ * stream's graphs in turn leaves the last stream idle for the others' launches.  The
+ * launcher keeps `threads - 1` worker threads (the caller is thread 0); stream s's graphs
+ * graphs[offs[s] .. offs[s+1]) (hipGraphExec_t) are launched in order on streams[s] (hipStream_t) by
+ * thread s % threads.  dkg_launcher_graphs returns once every launch call has returned.  Armed
+ * workers spin (wake-up in ~1 us) for `seconds`; otherwise they sleep on a condition variable.
+ * Host-side scheduling only (the reference has no counterpart: its forward is a Python loop,
+ * discretekg.py:145-159); no kernel is launched that the caller did not capture. */
+int dkg_launcher_create(int threads, void** launcher);
+int dkg_launcher_arm(void* launcher, double seconds);
+int dkg_launcher_graphs(void* launcher, int n_streams, void* const* streams, const int* offs,
+                        void* const* graphs);
+int dkg_launcher_destroy(void* launcher);
+
 #ifdef __cplusplus
 }
 #endif

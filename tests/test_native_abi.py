@@ -132,3 +132,21 @@ def test_f32_plan_flag_validation_without_device():
     assert st == _lib.DKG_ERR_UNSUPPORTED and b"forward only" in lib.dkg_last_error()
     st = lib.dkg_plan_init(outs, 2, 2, 16, 1024, 16, 16, -1, 128, 64, 16, 1 << 40, host, 16, None)
     assert st == _lib.DKG_ERR_ARG and b"unknown plan flags" in lib.dkg_last_error()
+
+
+def test_launcher_lifecycle_and_argument_checks():
+    """dkg_launcher_*: worker threads start and stop, an empty launch set returns, bad arguments are refused
+    (no graph is launched without a device)."""
+    from dkg_amd.launch import GraphLauncher
+
+    lib = _lib.load()
+    L = GraphLauncher(3)
+    L.arm(0.005)
+    L.prepare("empty", [], [])
+    L.launch("empty")
+    offs = (ctypes.c_int * 2)(1, 0)  # decreasing offsets
+    one = (ctypes.c_void_p * 1)(0)
+    assert lib.dkg_launcher_graphs(L._h, 1, one, offs, one) == _lib.DKG_ERR_ARG
+    L.close()
+    h = ctypes.c_void_p()
+    assert lib.dkg_launcher_create(0, ctypes.byref(h)) == _lib.DKG_ERR_ARG
