@@ -59,6 +59,7 @@ struct WsLayout {
   size_t wg_gpart;
   size_t tickets;
   size_t hull_pairs;
+  size_t icpt, itop, itopk;  // 0: none (streaming envelope)
   size_t total;
 };
 
@@ -132,6 +133,14 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
   off = align256(off + Bp * sizeof(int));
   L.hull_pairs = off;
   off = align256(off + (size_t)std::max(B, 1) * std::max(S, 1) * sizeof(int));
+  if (N + 1 <= 64 * 33) {  // the staged forward's intercept cache (Plan::icpt)
+    L.icpt = off;
+    off = align256(off + (size_t)std::max(S, 1) * 64 * env_slots(N + 1) * sizeof(double));
+    L.itop = off;
+    off = align256(off + (size_t)std::max(S, 1) * sizeof(double));
+    L.itopk = off;
+    off = align256(off + (size_t)std::max(S, 1) * 2 * sizeof(int));
+  }
   L.total = off;
   return L;
 }
@@ -231,6 +240,13 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
   P->wg_gpart = reinterpret_cast<double*>(ws + L.wg_gpart);
   P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
+  // the intercept cache serves the staged forward envelope (a gradient plan's forward included)
+  if (L.icpt && !stream) {
+    P->icpt = reinterpret_cast<double*>(ws + L.icpt);
+    P->icpt_stride = 64 * env_slots(N + 1);
+    P->itop = reinterpret_cast<double*>(ws + L.itop);
+    P->itopk = reinterpret_cast<int*>(ws + L.itopk);
+  }
   static const char* denv = std::getenv("DKG_DEBUG_ENV_FLAGS");
   static const char* dcov = std::getenv("DKG_DEBUG_COV_FLAGS");
   P->debug_env = (denv ? std::atoi(denv) : 0) | ((flags & DKG_PLAN_FORCE_WALK) ? 1 : 0) |
@@ -315,6 +331,7 @@ int copy_disc_means(const Plan& P, hipStream_t s) {
     if (P.grad && (st = hip_check(launch_unpack_rows(P.o[i].disc_frag, P.N, P.o[i].n, P.qdrm[i], s), "unpack_rows")))
       return st;
   }
+  if (P.icpt) return hip_check(launch_intercepts(P, s), "intercepts");
   return DKG_OK;
 }
 

@@ -321,6 +321,15 @@ __device__ __forceinline__ double readlane_f64(double v, int l);
 
 // A wave-uniform double moved to SGPRs (v_readfirstlane of both halves), so
 // it takes no VGPRs while it stays live.
+// A wave-uniform pointer to global memory, held in SGPRs: loads from it take the scalar-base form
+// (global_load ... v_offset, s[base]) with one VGPR offset, instead of a 64-bit VGPR address per load.
+typedef const __attribute__((address_space(1))) double* gdptr;
+__device__ __forceinline__ gdptr uniform_gptr(const double* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<gdptr>(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ double sgpr_f64(double v) {
   return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
                           __builtin_amdgcn_readfirstlane(__double2loint(v)));
@@ -408,6 +417,22 @@ __device__ __forceinline__ double psi(double c) {
   }
   const double r = e * g;
   return (c < 0.0) ? r + x : r;
+}
+
+// ---------------------------------------------------------------------------
+// XCD grouping of a launch (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement": workgroups are dealt
+// round-robin over the 8 XCDs, so ids L and L + 8 share one; a speed matter only, never correctness).  A
+// 1-D launch of xcd_group_size(nblk, groups) workgroups gives the `groups` members of block blk the ids
+// 8 (q groups + member) + blk % 8 (q = blk / 8): they are dispatched one after another to one XCD and
+// share its L2 -- the outputs of one covariance block write the same line records (whole records leave L2
+// instead of one component per write-back), the workgroups of one candidate's envelope read the same
+// records (one HBM read instead of one per workgroup).  False for the padding ids (blk >= nblk).
+__host__ __device__ inline int xcd_group_size(int nblk, int groups) { return 8 * groups * ((nblk + 7) / 8); }
+__device__ __forceinline__ bool xcd_group(int L, int nblk, int groups, int& blk, int& member) {
+  const int r = L >> 3;
+  member = r % groups;
+  blk = (r / groups) * 8 + (L & 7);
+  return blk < nblk;
 }
 
 // ---------------------------------------------------------------------------

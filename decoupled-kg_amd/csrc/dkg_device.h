@@ -388,18 +388,40 @@ __device__ __forceinline__ int first_max_index(const double (&la)[MAXL], int nl,
 // again only for a second filter or the walk over all lines, so no register
 // line is live across the list walk.  force_walk: test hook (every set takes
 // the walk over all lines).  pst (debug, DKG_DEBUG_STAMPS=2): phase stamps.
-template <int MAXL, class Build>
+// T (max a, tie: min b) known before the lines are in registers (the staged forward's plan keeps each
+// scalarisation's largest intercept over k >= 1: Plan::itop): valid when it is decided without a tie
+// (line 0 strictly above every other line, or one line k >= 1 strictly above the rest, line 0 included).
+struct TopHint {
+  bool valid;
+  double aT, bT;
+};
+
+template <int MAXL, class Build, class Build0 = int>
 __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
                                                 bool force_walk, int* nhull, const WalkOut* out = nullptr,
-                                                unsigned long long* pst = nullptr, bool flat_ok = false) {
+                                                unsigned long long* pst = nullptr, bool flat_ok = false,
+                                                const Build0* build0 = nullptr,
+                                                TopHint hint = TopHint{false, 0.0, 0.0}) {
   FwdEnv f;
   if (pst) pst[0] = __builtin_amdgcn_s_memtime();
   {
     double la[MAXL], lb[MAXL];
-    build(la, lb);
+    if constexpr (std::is_same_v<Build0, int>) {
+      build(la, lb);
+    } else {
+      (*build0)(la, lb);  // the first build (e.g. from registers loaded ahead)
+    }
     if (pst) pst[1] = __builtin_amdgcn_s_memtime();
-    if (flat_ok) {
+    if (flat_ok && hint.valid) {
+      f.aT = hint.aT;  // what env_top finds, without its two wave reductions
+      f.bT = hint.bT;
+      f.aL = f.aR = -INFINITY;
+      f.cnt = 0;
+      f.status = 0;
+    } else if (flat_ok) {
       env_top<MAXL>(la, lb, f);
+    }
+    if (flat_ok) {
       if (pst) pst[2] = __builtin_amdgcn_s_memtime();
       if (env_flat<MAXL>(la, lb, f)) {
         *nhull = 0;  // not walked: KG_w = 0 exactly (env_flat)
@@ -476,11 +498,14 @@ __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, in
 }
 
 // KG_w of register-held lines (env_pair_regs_edges), with the single psi evaluation of its edge terms.
-template <int MAXL, class Build>
+template <int MAXL, class Build, class Build0 = int>
 __device__ __forceinline__ double env_pair_regs(Build&& build, int nl, int lane, double* sb, double* sa, int* si,
                                                 bool force_walk, int* nhull, const WalkOut* out = nullptr,
-                                                unsigned long long* pst = nullptr, bool flat_ok = false) {
-  return finish_edges(env_pair_regs_edges<MAXL>(build, nl, lane, sb, sa, si, force_walk, nhull, out, pst, flat_ok));
+                                                unsigned long long* pst = nullptr, bool flat_ok = false,
+                                                const Build0* build0 = nullptr,
+                                                TopHint hint = TopHint{false, 0.0, 0.0}) {
+  return finish_edges(
+      env_pair_regs_edges<MAXL>(build, nl, lane, sb, sa, si, force_walk, nhull, out, pst, flat_ok, build0, hint));
 }
 
 // ---------------------------------------------------------------------------
@@ -1232,11 +1257,6 @@ __device__ __forceinline__ void pair_coefs(const double* wrow, int m, bool full,
 // Padded length (doubles) of one LDS-staged line array: whole 1 KiB DMA pieces.
 __host__ __device__ inline int stage_len(int N) { return ((N + 127) / 128) * 128; }
 
-// Register slots per lane for a staged (non-streaming) line set of `lines`
-// lines: the envelope_kernel instantiation launch_env_bucket picks.
-__host__ __device__ inline int env_slots(int lines) {
-  return lines <= 64 * 2 ? 2 : lines <= 64 * 8 ? 8 : lines <= 64 * 17 ? 17 : 33;
-}
 
 // Doubles in front of a staged record array: line 0 (the candidate, built from
 // registers) reads record -1 there.
@@ -1335,8 +1355,10 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   constexpr int MP = cov_rec(M);  // doubles per line record
   const int SLp = STREAM ? 0 : stage_stride(N, MP);
   constexpr int LC = list_cap(STREAM && !GRAD);  // survivor-list capacity per wave
+  // (the staged forward without mu_D records: its covariance records start where they would)
+  constexpr bool MU_STAGED = GRAD || HO;
   double* lmu = smem + STAGE_FRONT;
-  double* lcv = lmu + SLp;
+  double* lcv = lmu + ((STREAM || MU_STAGED) ? SLp : 0);
   double* lw = lcv + SLp;
   double* skg = lw + ((S * m + 1) & ~1);  // KG_j of the group's pairs (summed in j order)
   double* sbuf = skg + ((S + 1) & ~1);
@@ -1387,7 +1409,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   }
   const double* wsrc = wts;
   if constexpr (!STREAM) {
-    dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
+    // (the staged forward reads its intercepts from the plan's cache instead: no mu_D records in LDS)
+    if constexpr (GRAD || HO) dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
     if constexpr (!HO) dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
   }
   if constexpr (GRAD) {
@@ -1444,13 +1467,27 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   const int pad_end = (64 * MAXL - 1) * MP;
   auto pad_lines = [&](int lo, int hi) {  // doubles lo .. hi-1 of both record arrays
     for (int e = lo + (int)threadIdx.x; e < hi; e += blockDim.x) {
-      lmu[e] = __builtin_nan("");
+      if constexpr (GRAD || HO) lmu[e] = __builtin_nan("");
       lcv[e] = __builtin_nan("");
     }
   };
   if constexpr (!STREAM) pad_lines(max(N * MP, SLd), pad_end);
   // pairs j0 .. j1-1 of the candidate, one per wave (gridDim.y = ceil(S / SW), envelope_geometry)
   const int j0 = g * SW, j1 = min(S, j0 + SW);
+  // Staged forward with the plan's intercept cache (Plan::icpt): this wave's intercepts a_k (slot t of lane
+  // l: line l + 64 t) straight into registers, in flight with the staging DMA; only the covariance records
+  // are built from LDS.
+  constexpr bool ICP = !GRAD && !STREAM && !HO;
+  gdptr icp = nullptr;  // this wave's row of the cache (wave-uniform)
+  double ila[ICP ? MAXL : 1];
+  if constexpr (ICP) {
+    // always set for a staged plan (dkg_abi.hip build_plan)
+    icp = uniform_gptr(P->icpt + (size_t)min(j0 + wave, S - 1) * P->icpt_stride);
+    if (j0 + wave < j1) {
+#pragma unroll
+      for (int t = 0; t < MAXL; ++t) ila[t] = icp[lane_k + 64 * t];
+    }
+  }
   if (!GRAD) KST(st, 2);  // GRAD stamps: 2 preamble done, 3 filter, 4 hull, 5 gradient flush (first pair)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2161,14 +2198,102 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     } else if constexpr (STREAM) {
       kgj = env_pair_stream<MAXL>(nch, NL, lane, sb, sa, sif, vreg, force_walk, &hn, build_chunk);
     } else {
-      // the lines are rebuilt from the staged LDS data if the list walk cannot finish,
-      // so no register line is live across it
-      auto rebuild = [&](double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
       unsigned long long* pst = (dst == 2 && lane == 0 && (size_t)b * S + j < 2 * KST_WG)
                                     ? P->kstamps + ((size_t)b * S + j) * 8 : nullptr;
       // pairs_out also records the envelope size: every pair is walked then
-      kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst,
-                                pairs_out == nullptr && !force_walk);
+      const bool flat_ok = pairs_out == nullptr && !force_walk;
+      if constexpr (ICP) {
+        // intercepts from the plan (first build: the registers loaded ahead; a rebuild: global memory)
+        auto slopes = [&](double (&lb)[MAXL]) {
+          const double* cvr = lcv + (lane - 1) * MP;
+          if (full) {
+#pragma unroll
+            for (int t = 0; t < MAXL; ++t) {
+              double acc = 0.0;  // build_lines' rec_dot of the covariance record
+              if constexpr (MP == 1) {
+                acc = fma(wb[0], cvr[64 * MP * t], acc);
+              } else {
+#pragma unroll
+                for (int q = 0; 2 * q < M; ++q) {
+                  const double2 u = *reinterpret_cast<const double2*>(cvr + 64 * MP * t + 2 * q);
+                  acc = fma(wb[2 * q], u.x, acc);
+                  if (2 * q + 1 < M) acc = fma(wb[2 * q + 1], u.y, acc);
+                }
+              }
+              lb[t] = acc;
+            }
+          } else {
+            double wbt = 0.0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
+#pragma unroll
+            for (int t = 0; t < MAXL; ++t) lb[t] = wbt * cvr[64 * MP * t + target];
+          }
+          double a = a_off, bb = 0.0;  // line 0: the candidate itself (discretekg.py:182-183)
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            a = fma(wa[i], mx0[i], a);
+            bb = fma(wb[i], sv[i], bb);
+          }
+          lb[0] = (lane == 0) ? bb : lb[0];
+          return a;
+        };
+        auto first = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
+          const double a0 = slopes(lb);
+#pragma unroll
+          for (int t = 0; t < MAXL; ++t) la[t] = ila[t];
+          la[0] = (lane == 0) ? a0 : la[0];
+        };
+        auto again = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
+          const double a0 = slopes(lb);
+#pragma unroll
+          for (int t = 0; t < MAXL; ++t) la[t] = icp[lane + 64 * t];
+          la[0] = (lane == 0) ? a0 : la[0];
+        };
+        // T without a wave reduction when the plan's top intercept decides it (TopHint)
+        TopHint hint{false, 0.0, 0.0};
+        if (flat_ok) {
+          double a0 = a_off, b0 = 0.0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            a0 = fma(wa[i], mx0[i], a0);
+            b0 = fma(wb[i], sv[i], b0);
+          }
+          const double A1 = P->itop[j];
+          const int k1 = P->itopk[2 * j], c1 = P->itopk[2 * j + 1];
+          if (a0 > A1) {
+            hint = TopHint{true, a0, b0};
+          } else if (a0 < A1 && c1 == 1) {
+            // line k1's slope, as the build computes it (record k1 - 1)
+            const double* r = lcv + (size_t)(k1 - 1) * MP;
+            double bk = 0.0;
+            if (full) {
+              if constexpr (MP == 1) {
+                bk = fma(wb[0], r[0], bk);
+              } else {
+#pragma unroll
+                for (int q = 0; 2 * q < M; ++q) {
+                  const double2 u = *reinterpret_cast<const double2*>(r + 2 * q);
+                  bk = fma(wb[2 * q], u.x, bk);
+                  if (2 * q + 1 < M) bk = fma(wb[2 * q + 1], u.y, bk);
+                }
+              }
+            } else {
+              double wbt = 0.0;
+#pragma unroll
+              for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
+              bk = wbt * r[target];
+            }
+            hint = TopHint{true, A1, bk};
+          }
+        }
+        kgj = env_pair_regs<MAXL>(again, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst, flat_ok, &first, hint);
+      } else {
+        // the lines are rebuilt from the staged LDS data if the list walk cannot finish,
+        // so no register line is live across it
+        auto rebuild = [&](double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
+        kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst, flat_ok);
+      }
     }
     if (pairs_out != nullptr && lane == 0) {
       pairs_out[(size_t)b * S + j] = kgj;
@@ -2284,12 +2409,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ var_all,
                                                        const double* __restrict__ mux_all,
                                                        const double* __restrict__ wts, long long cov_stride,
-                                                       int bpad, double* __restrict__ hout) {
+                                                       int bpad, double* __restrict__ hout, int split) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
+  // 1-D grid: the `split` workgroups of one candidate side by side on one XCD (xcd_group), so its line
+  // records come from HBM once and from that XCD's L2 for the others
+  int b, g;
+  if (!xcd_group(blockIdx.x, B, split, b, g)) return;
   envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
-                                       cov_stride, bpad, blockIdx.x, blockIdx.y, gridDim.y, smem, kst_slot(dst, P, 2),
-                                       nullptr, hout);
+                                       cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout);
 }
 
 // The lines of every (candidate, scalarisation) pair of the plan's last
@@ -2366,7 +2494,7 @@ hipError_t launch_env_t(const EnvLaunch& a) {
   const Plan& h = *a.host;
   hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights,
-                     (long long)h.cov_stride, h.bpad, a.hout);
+                     (long long)h.cov_stride, h.bpad, a.hout, h.split);
   return hipGetLastError();
 }
 

@@ -33,6 +33,12 @@ __host__ __device__ constexpr int cov_rec(int m) { return m <= 1 ? 1 : m <= 2 ? 
 #endif
 __host__ __device__ inline bool cross_kfill(int np) { return DKG_CROSS_KFILL && np >= 512; }
 
+// Register slots per lane for a staged (non-streaming) line set of `lines`
+// lines: the envelope_kernel instantiation launch_env_bucket picks.
+__host__ __device__ inline int env_slots(int lines) {
+  return lines <= 64 * 2 ? 2 : lines <= 64 * 8 ? 8 : lines <= 64 * 17 ? 17 : 33;
+}
+
 struct Plan {
   dkg_output o[DKG_MAX_OUTPUTS];
   int32_t m, d, N, S, target;       // target < 0: all outputs observed
@@ -72,6 +78,13 @@ struct Plan {
   unsigned long long* sync;         // fused hand-off counters: cnt1 [m][rt], cnt2 [nrb], done (zeroed)
   int* sync_err;                    // fused waits that gave up (bits), after the counters
   size_t sync_bytes;                // bytes of the counter block (sync .. sync_err), a multiple of 16
+  // Staged forward: the intercepts of lines k >= 1 depend on the weights and mu_D only, not on the
+  // candidates -- a_k = a_off + sum_i w_i sd_i mu_i(z_k), discretekg.py:201-213 -- so the plan keeps them
+  // (dkg_plan_init, the envelope's own arithmetic: bit-identical lines) beside each scalarisation's largest.
+  double* icpt;                     // [S][icpt_stride]: slot k = a_k for 1 <= k <= N, NaN at k = 0 and k > N
+  int32_t icpt_stride;              // 64 * env_slots(N + 1): one entry per register slot of the envelope
+  double* itop;                     // [S]: max_{k >= 1} a_k (-inf when N = 0)
+  int* itopk;                       // [S][2]: the first k >= 1 attaining it, and how many lines do
 };
 
 // By-value arguments of the state-preparation use of the cross stage.
@@ -107,6 +120,8 @@ hipError_t launch_alpha(const double* X, const double* y, double c, int n, doubl
 hipError_t launch_pack_linv(const double* X, int n, double* rf, hipStream_t s);
 // fp32 quad-packed copy (frag32_index) of a pair-packed fp64 (rows x n) matrix.
 hipError_t launch_frag_to_f32(const double* frag, int rows, int n, float* out, hipStream_t s);
+// The plan's per-scalarisation intercepts and their maxima (Plan::icpt / itop / itopk), from mu_all.
+hipError_t launch_intercepts(const Plan& h, hipStream_t s);
 // Row-major copy [rows][n_pad] of a fragment-packed (rows x n) matrix.
 hipError_t launch_unpack_rows(const double* frag, int rows, int n, double* out, hipStream_t s);
 hipError_t launch_cross_root(const CrossArgs& a, hipStream_t s);
@@ -150,7 +165,9 @@ hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStr
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and
 // workgroups per candidate.
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow);
-size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad = false);
+// mu: the mu_D records are staged too (the gradient and fused envelopes; the staged forward reads the plan's
+// intercept cache instead)
+size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad = false, bool mu = true);
 size_t cross_root_lds_bytes(int np, int d);
 
 }  // namespace dkg

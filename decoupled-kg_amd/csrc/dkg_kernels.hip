@@ -69,6 +69,111 @@ __global__ void frag_to_f32_kernel(const double* __restrict__ frag, int rows_pad
 }
 
 
+// Plan init (staged forward): every scalarisation's intercepts a_k, k >= 1, with the envelope's own
+// arithmetic (pair_coefs' a_off and w_i sd_i, build_lines' record dot in output order: the same bits as the
+// lines the envelope used to build), NaN in slot 0 and past N; then their maximum over k >= 1 and the first
+// k attaining it with the number of lines that do.  One workgroup per scalarisation.
+struct IcptArgs {
+  const double* mu_all;
+  const double* weights;
+  double* icpt;
+  double* itop;
+  int* itopk;
+  int m, N, stride;
+  double ysd[DKG_MAX_OUTPUTS], ymu[DKG_MAX_OUTPUTS];
+};
+
+template <int M>
+__global__ __launch_bounds__(256) void intercepts_kernel(IcptArgs a) {
+  __shared__ double smax[256];
+  __shared__ int sfirst[256], scount[256];
+  constexpr int MP = cov_rec(M);
+  const int j = blockIdx.x, m = a.m;
+  double w[M], wa[M], a_off = 0.0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const bool live = i < m;
+    w[i] = live ? a.weights[(size_t)j * m + i] : 0.0;
+    wa[i] = w[i] * (live ? a.ysd[i] : 1.0);
+    a_off = fma(w[i], live ? a.ymu[i] : 0.0, a_off);
+  }
+  double* out = a.icpt + (size_t)j * a.stride;
+  double mx = -INFINITY;
+  for (int k = threadIdx.x; k < a.stride; k += blockDim.x) {
+    double v = __builtin_nan("");
+    if (k >= 1 && k <= a.N) {
+      const double* r = a.mu_all + (size_t)(k - 1) * MP;
+      double acc = a_off;
+      if constexpr (MP == 1) {
+        acc = fma(wa[0], r[0], acc);
+      } else {
+#pragma unroll
+        for (int q = 0; 2 * q < M; ++q) {
+          acc = fma(wa[2 * q], r[2 * q], acc);
+          if (2 * q + 1 < M) acc = fma(wa[2 * q + 1], r[2 * q + 1], acc);
+        }
+      }
+      v = acc;
+      mx = fmax(mx, v);
+    }
+    out[k] = v;
+  }
+  smax[threadIdx.x] = mx;
+  __syncthreads();
+  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) smax[threadIdx.x] = fmax(smax[threadIdx.x], smax[threadIdx.x + h]);
+    __syncthreads();
+  }
+  const double top = smax[0];
+  int first = 0x7fffffff, count = 0;
+  for (int k = threadIdx.x; k < a.stride; k += blockDim.x) {
+    if (k >= 1 && k <= a.N && out[k] == top) {
+      first = min(first, k);
+      ++count;
+    }
+  }
+  sfirst[threadIdx.x] = first;
+  scount[threadIdx.x] = count;
+  __syncthreads();
+  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      sfirst[threadIdx.x] = min(sfirst[threadIdx.x], sfirst[threadIdx.x + h]);
+      scount[threadIdx.x] += scount[threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.itop[j] = top;
+    a.itopk[2 * j] = scount[0] > 0 ? sfirst[0] : 0;
+    a.itopk[2 * j + 1] = scount[0];
+  }
+}
+
+hipError_t launch_intercepts(const Plan& h, hipStream_t s) {
+  IcptArgs a{};
+  a.mu_all = h.mu_all;
+  a.weights = h.weights;
+  a.icpt = h.icpt;
+  a.itop = h.itop;
+  a.itopk = h.itopk;
+  a.m = h.m;
+  a.N = h.N;
+  a.stride = h.icpt_stride;
+  for (int i = 0; i < h.m; ++i) {
+    a.ysd[i] = h.o[i].y_std;
+    a.ymu[i] = h.o[i].y_mean;
+  }
+  const dim3 grid(h.S), block(256);
+  switch (h.m <= 1 ? 1 : h.m <= 2 ? 2 : h.m <= 3 ? 3 : h.m <= 4 ? 4 : 8) {
+    case 1: hipLaunchKernelGGL(intercepts_kernel<1>, grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(intercepts_kernel<2>, grid, block, 0, s, a); break;
+    case 3: hipLaunchKernelGGL(intercepts_kernel<3>, grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL(intercepts_kernel<4>, grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL(intercepts_kernel<8>, grid, block, 0, s, a); break;
+  }
+  return hipGetLastError();
+}
+
 template <int DM>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -158,9 +263,9 @@ size_t cross_root_lds_bytes(int np, int d) { return cross_lds_doubles(np, d, cro
 
 static int outputs_bucket(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 3 ? 3 : m <= 4 ? 4 : 8; }
 
-size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad) {
+size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad, bool mu) {
   const int M = outputs_bucket(m);
-  const size_t staged = stream ? 0 : 2 * (size_t)stage_stride(N, cov_rec(M));
+  const size_t staged = stream ? 0 : (mu ? 2 : 1) * (size_t)stage_stride(N, cov_rec(M));
   const bool refine = stream && !grad;  // streaming forward: long lists + quickhull vertex arrays
   const size_t lc = list_cap(refine);
   // per wave: the list (slopes, intercepts; forward: line indices) and the streaming vertex arrays
@@ -168,7 +273,8 @@ size_t envelope_lds_bytes(int m, int N, int waves, int S, bool stream, bool grad
   const size_t vroom = !refine ? 0
                        : stream_staged(M) ? std::max((size_t)waves * VREG, (size_t)4 * staged_chunk_len(cov_rec(M)))
                                           : (size_t)waves * VREG;
-  return ((size_t)2 + staged + ((S * m + 1) & ~1) + ((S + 1) & ~1) + (size_t)waves * 2 * lc + vroom +
+  // the kernel's layout (envelope_body): STAGE_FRONT doubles, the staged arrays, weights, pair sums, lists
+  return ((size_t)STAGE_FRONT + staged + ((S * m + 1) & ~1) + ((S + 1) & ~1) + (size_t)waves * 2 * lc + vroom +
           (grad ? 0 : ((size_t)waves * lc + 1) / 2)) * sizeof(double);
 }
 
@@ -375,13 +481,13 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
   }
   if constexpr (sizeof(T) == 8 && DM <= 4) {
     if (cov_wide(h.N, B, h.m)) {
-      dim3 grid((h.N + 63) / 64, (B + 63) / 64, h.m);
+      dim3 grid(xcd_group_size(((h.N + 63) / 64) * ((B + 63) / 64), h.m));
       hipLaunchKernelGGL((posterior_cov_wide_kernel<DM>), grid, dim3(PW_WAVES * WAVE), 0, s, dev, xnew, B,
                          h.debug_stamp);
       return hipGetLastError();
     }
   }
-  dim3 grid(std::max(1, (h.N + 31) / 32), (B + 16 * PC_RB - 1) / (16 * PC_RB), h.m);
+  dim3 grid(xcd_group_size(std::max(1, (h.N + 31) / 32) * ((B + 16 * PC_RB - 1) / (16 * PC_RB)), h.m));
   hipLaunchKernelGGL((posterior_cov_kernel<DM, T>), grid, dim3(PC_WAVES * WAVE), 0, s, dev, xnew, B, h.debug_stamp);
   return hipGetLastError();
 }
@@ -432,8 +538,9 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
       default: return launch_cross_cov_t<16>(h, dev, xnew, B, kg, s, stage);
     }
   }
-  EnvLaunch a{&h, dev, B, kg, pairs, dim3(B, h.split), dim3(h.sw * WAVE),
-              envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0), s, h.debug_stamp, nullptr, nullptr};
+  EnvLaunch a{&h, dev, B, kg, pairs, dim3(xcd_group_size(B, h.split)), dim3(h.sw * WAVE),
+              envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0, false, false), s, h.debug_stamp, nullptr,
+              nullptr};
   return launch_env<false>(h, a);
 }
 
@@ -462,7 +569,7 @@ hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xne
   }
   if (e != hipSuccess) return e;
   if ((e = launch_stage(h, dev, xnew, B, kg, nullptr, s, 1)) != hipSuccess) return e;  // cov rows, variances
-  EnvLaunch a{&h, dev, B, kg, nullptr, dim3(B, h.split), dim3(h.sw * WAVE),
+  EnvLaunch a{&h, dev, B, kg, nullptr, dim3(xcd_group_size(B, h.split)), dim3(h.sw * WAVE),
               envelope_grad_lds_bytes(h.m, h.N, h.sw, h.S, h.d, h.max_np, h.stream != 0), s, h.debug_stamp, xnew, dkg,
               hout};
   return launch_env<true>(h, a);

@@ -561,17 +561,21 @@ __global__ __launch_bounds__(PW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
                                                                              int B, int dst) {
   __shared__ __attribute__((aligned(16))) double part[2 * 4 * 2 * 4 * 64];  // [row tile][sub-block][col tile] sums
   __shared__ double qpart[2 * 4 * 16];                                      // [row tile][sub-block] |Q_X|^2 sums
+  // 1-D grid, the outputs of one 64 x 64 block side by side on one XCD (xcd_group)
+  const int N = P->N;
+  const int nbx = (N + 63) / 64, nby = (B + 63) / 64;
+  int blk, oi;
+  if (!xcd_group(blockIdx.x, nbx * nby, P->m, blk, oi)) return;
   unsigned long long* st = kst_slot(dst, P, 1);
   KST_BEGIN(st);
-  const int oi = blockIdx.z;
+  const int bx = blk % nbx, by = blk / nbx;
   const dkg_output& o = P->o[oi];
-  const int N = P->N;
   const int d = P->d;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int sb = wave & 3, ks = wave >> 2;
-  const int ti0 = 4 * blockIdx.y + 2 * (sb >> 1);  // row tiles ti0, ti0 + 1
-  const int tk0 = 4 * blockIdx.x + 2 * (sb & 1);   // column tiles tk0, tk0 + 1
+  const int ti0 = 4 * by + 2 * (sb >> 1);  // row tiles ti0, ti0 + 1
+  const int tk0 = 4 * bx + 2 * (sb & 1);   // column tiles tk0, tk0 + 1
   const int RT = pad16(B) / 16, CT = pad16(N) / 16;  // tiles that exist
   const int KB = pad16(o.n) / 4;
   const int KP = KB / 2;  // 16-byte words (two k-blocks each)
@@ -673,7 +677,11 @@ __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Pl
   __shared__ double qpart[(PC_KS - 1) * 2 * PC_RB * 16];
   unsigned long long* st = kst_slot(dst, P, 1);
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 1)) return;  // ablation: empty covariance stage
-  posterior_cov_body<DM, T>(P, xnew, B, blockIdx.x, blockIdx.y, blockIdx.z, part, qpart, st);
+  // 1-D grid, the outputs of one 32 x 32 block side by side on one XCD (xcd_group)
+  const int nbx = max(1, (P->N + 31) / 32), nby = (B + 16 * PC_RB - 1) / (16 * PC_RB);
+  int blk, oi;
+  if (!xcd_group(blockIdx.x, nbx * nby, P->m, blk, oi)) return;
+  posterior_cov_body<DM, T>(P, xnew, B, blk % nbx, blk / nbx, oi, part, qpart, st);
 }
 
 }  // namespace dkg
