@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--graph-head", type=int, default=1,
                     help="--graph 2: each stream's period graph split into its first GRAPH_HEAD forwards and the rest, "
                          "the heads of all streams launched first (0 = one graph per stream)")
-    ap.add_argument("--launch-threads", type=int, default=-1,
+    ap.add_argument("--launch-threads", type=int, default=1,
                     help="--graph 2: host threads enqueuing the streams' graphs side by side (dkg_launcher; "
                          "-1 = one per stream, 1 = the caller alone, in stream order)")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")

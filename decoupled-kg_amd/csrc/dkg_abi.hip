@@ -58,6 +58,7 @@ struct WsLayout {
   size_t wg_part;
   size_t wg_gpart;
   size_t tickets;
+  size_t dup;
   size_t hull_pairs;
   size_t icpt, itop, itopk;  // 0: none (streaming envelope)
   size_t total;
@@ -124,12 +125,14 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
   int sw, split;
   envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split, !(flags & DKG_PLAN_FUSED));
   // split > 1: every pair's KG (and, value+gradient, its dKG/dx) for the last workgroup's ordered sums
+  const size_t pcols = (size_t)std::max(S, 1) + pair_groups(std::max(S, 1));  // pair values + group terms
   L.wg_part = off;
-  off = align256(off + (split > 1 ? (size_t)std::max(B, 1) * std::max(S, 1) * sizeof(double) : 0));
+  off = align256(off + (split > 1 ? (size_t)std::max(B, 1) * pcols * sizeof(double) : 0));
   L.wg_gpart = off;
-  off = align256(off + ((flags & DKG_PLAN_GRAD) && split > 1 ? (size_t)std::max(B, 1) * std::max(S, 1) * d * sizeof(double)
-                                                             : 0));
+  off = align256(off + ((flags & DKG_PLAN_GRAD) && split > 1 ? (size_t)std::max(B, 1) * pcols * d * sizeof(double) : 0));
   L.tickets = off;
+  off = align256(off + Bp * (pair_groups(std::max(S, 1)) + 1) * sizeof(int));
+  L.dup = off;
   off = align256(off + Bp * sizeof(int));
   L.hull_pairs = off;
   off = align256(off + (size_t)std::max(B, 1) * std::max(S, 1) * sizeof(int));
@@ -238,6 +241,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->cov_stride = (int64_t)std::max(N, 1) * cov_rec(m);
   P->wg_part = reinterpret_cast<double*>(ws + L.wg_part);
   P->tickets = reinterpret_cast<int*>(ws + L.tickets);
+  P->dup = reinterpret_cast<int*>(ws + L.dup);
   P->wg_gpart = reinterpret_cast<double*>(ws + L.wg_gpart);
   P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
   // the intercept cache serves the staged forward envelope (a gradient plan's forward included)

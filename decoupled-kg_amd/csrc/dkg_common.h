@@ -427,8 +427,20 @@ __device__ __forceinline__ double psi(double c) {
 // share its L2 -- the outputs of one covariance block write the same line records (whole records leave L2
 // instead of one component per write-back), the workgroups of one candidate's envelope read the same
 // records (one HBM read instead of one per workgroup).  False for the padding ids (blk >= nblk).
-__host__ __device__ inline int xcd_group_size(int nblk, int groups) { return 8 * groups * ((nblk + 7) / 8); }
+// DKG_XCD_GROUP=0 (A/B only: profiles/r04/abv, 9.95 against 10.2 M KG-evals/s with four forwards in flight): the ids
+// follow the 2-D order (member-major, blk = L % nblk), every block's members on different XCDs.
+#ifndef DKG_XCD_GROUP
+#define DKG_XCD_GROUP 1
+#endif
+__host__ __device__ inline int xcd_group_size(int nblk, int groups) {
+  return DKG_XCD_GROUP ? 8 * groups * ((nblk + 7) / 8) : nblk * groups;
+}
 __device__ __forceinline__ bool xcd_group(int L, int nblk, int groups, int& blk, int& member) {
+  if (!DKG_XCD_GROUP) {
+    blk = L % nblk;
+    member = L / nblk;
+    return true;
+  }
   const int r = L >> 3;
   member = r % groups;
   blk = (r / groups) * 8 + (L & 7);

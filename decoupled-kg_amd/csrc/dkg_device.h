@@ -65,6 +65,12 @@ __device__ __forceinline__ unsigned long long* kst_slot(int dst, const Plan* P, 
 constexpr int ENV_CAP = 128;
 constexpr int HCAP = 128;  // GRAD: queued envelope lines per wave before their gradient terms are flushed
 constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lines)
+// Staged forward: the intercepts from the plan's per-scalarisation cache (Plan::icpt) instead of the staged
+// mu_D records.  Off by default: the cache rows cost each wave 17 global loads per pair, and the envelope
+// was slower with them (profiles/r04/ab: 10.6 -> 11.0 us alone, 11.5 -> 9.9 M KG-evals/s with 4 streams).
+#ifndef DKG_ICP
+#define DKG_ICP 0
+#endif
 // Streaming forward with LDS-staged chunks (M = 2..4): the extremes and filter passes read the line
 // records from LDS, STAGED_SLOTS * 64 lines per chunk, double-buffered and shared by the workgroup's pairs.
 constexpr int STAGED_SLOTS = 8;
@@ -1320,12 +1326,15 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
                                               const double* __restrict__ mu_all, const double* __restrict__ cov_all,
                                               const double* __restrict__ var_all,
                                               const double* __restrict__ mux_all, const double* __restrict__ wts,
-                                              long long cov_stride, int bpad, int b, int g, int G, double* smem,
-                                              unsigned long long* st, const Handoff* ho = nullptr,
-                                              double* __restrict__ hout = nullptr) {
+                                              const int* __restrict__ dupv, long long cov_stride, int bpad, int b,
+                                              int g, int G, double* smem, unsigned long long* st,
+                                              const Handoff* ho = nullptr, double* __restrict__ hout = nullptr) {
   static_assert(!HO || (!GRAD && !STREAM), "the fused forward stages its lines (no gradient, no streaming)");
-  // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space)
-  __shared__ double s_pp[DKG_MAX_OUTPUTS * 6];
+  // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space),
+  // and line 0's inputs: the mean and slope component it is built from (x_b's own, or, when x_b coincides
+  // with a discretisation point (Plan::dup), that line's record: line 0 is then its exact copy)
+  constexpr int NPP = 8;
+  __shared__ double s_pp[DKG_MAX_OUTPUTS * NPP];
   __shared__ int s_kind[DKG_MAX_OUTPUTS];  // GRAD: covariance family per output
   const int SW = blockDim.x >> 6;
   const int lane_k = threadIdx.x & 63;
@@ -1356,7 +1365,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   const int SLp = STREAM ? 0 : stage_stride(N, MP);
   constexpr int LC = list_cap(STREAM && !GRAD);  // survivor-list capacity per wave
   // (the staged forward without mu_D records: its covariance records start where they would)
-  constexpr bool MU_STAGED = GRAD || HO;
+  constexpr bool ICP = DKG_ICP && !GRAD && !STREAM && !HO;  // intercepts from the plan's cache (Plan::icpt)
+  constexpr bool MU_STAGED = !ICP;
   double* lmu = smem + STAGE_FRONT;
   double* lcv = lmu + ((STREAM || MU_STAGED) ? SLp : 0);
   double* lw = lcv + SLp;
@@ -1393,7 +1403,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   // ---- one round of memory traffic: DMA the line data, plain loads for the rest
   // per-output scalars and the candidate's own posterior (variance from the
   // covariance stage, mean from the cross stage): lane i of wave 0 loads output i
-  double pp[6] = {1.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double pp[NPP] = {1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double g_gm[M], g_il[M], g_x = 0.0;  // GRAD: staged to LDS after the wait
   if (threadIdx.x < m) {
     const dkg_output* o = &P->o[threadIdx.x];
@@ -1404,13 +1414,15 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     if constexpr (!HO) {
       pp[4] = var_all[(size_t)threadIdx.x * bpad + b];
       pp[5] = mux_all[(size_t)threadIdx.x * bpad + b];
+      pp[6] = pp[5];
+      pp[7] = pp[4];
     }
     if constexpr (GRAD) s_kind[threadIdx.x] = o->kernel;
   }
   const double* wsrc = wts;
   if constexpr (!STREAM) {
     // (the staged forward reads its intercepts from the plan's cache instead: no mu_D records in LDS)
-    if constexpr (GRAD || HO) dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
+    if constexpr (MU_STAGED) dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
     if constexpr (!HO) dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
   }
   if constexpr (GRAD) {
@@ -1428,17 +1440,21 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     }
   }
   for (int e = threadIdx.x; e < S * m; e += blockDim.x) lw[e] = wsrc[e];
+  // candidate b's coincidence mark (the covariance stage's; loaded with the first batch, used after the wait)
+  int dupk = DUP_NONE;
+  if constexpr (!HO) dupk = dupv[b];
   if (threadIdx.x < m) {
 #pragma unroll
-    for (int q = 0; q < (HO ? 4 : 6); ++q) s_pp[threadIdx.x * 6 + q] = pp[q];
+    for (int q = 0; q < (HO ? 4 : NPP); ++q) s_pp[threadIdx.x * NPP + q] = pp[q];
   }
   if constexpr (HO) {
     // the candidate's row block of covariance rows (and, transitively, its cross stage's means) is out
     handoff_wait(ho->cnt2 + (size_t)(b / ho->rb_rows) * HANDOFF_STRIDE, 1, ho->quota2, ho->err, 2);
     if (threadIdx.x < m) {
-      s_pp[threadIdx.x * 6 + 4] = var_all[(size_t)threadIdx.x * bpad + b];
-      s_pp[threadIdx.x * 6 + 5] = mux_all[(size_t)threadIdx.x * bpad + b];
+      s_pp[threadIdx.x * NPP + 4] = s_pp[threadIdx.x * NPP + 7] = var_all[(size_t)threadIdx.x * bpad + b];
+      s_pp[threadIdx.x * NPP + 5] = s_pp[threadIdx.x * NPP + 6] = mux_all[(size_t)threadIdx.x * bpad + b];
     }
+    dupk = dupv[b];
     dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
   }
   if constexpr (GRAD) {
@@ -1467,7 +1483,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   const int pad_end = (64 * MAXL - 1) * MP;
   auto pad_lines = [&](int lo, int hi) {  // doubles lo .. hi-1 of both record arrays
     for (int e = lo + (int)threadIdx.x; e < hi; e += blockDim.x) {
-      if constexpr (GRAD || HO) lmu[e] = __builtin_nan("");
+      if constexpr (MU_STAGED) lmu[e] = __builtin_nan("");
       lcv[e] = __builtin_nan("");
     }
   };
@@ -1477,7 +1493,6 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   // Staged forward with the plan's intercept cache (Plan::icpt): this wave's intercepts a_k (slot t of lane
   // l: line l + 64 t) straight into registers, in flight with the staging DMA; only the covariance records
   // are built from LDS.
-  constexpr bool ICP = !GRAD && !STREAM && !HO;
   gdptr icp = nullptr;  // this wave's row of the cache (wave-uniform)
   double ila[ICP ? MAXL : 1];
   if constexpr (ICP) {
@@ -1496,6 +1511,14 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
       pad_lines(N * MP, min(SLd, pad_end));
       __syncthreads();
     }
+  }
+  dupk = __builtin_amdgcn_readfirstlane(dupk);
+  if (dupk != DUP_NONE) {  // rare (workgroup-uniform): line 0 from record dupk, the same bits as line dupk + 1
+    if (threadIdx.x < m) {
+      s_pp[threadIdx.x * NPP + 6] = mu_all[(size_t)dupk * MP + threadIdx.x];
+      s_pp[threadIdx.x * NPP + 7] = cov_all[(size_t)b * cov_stride + (size_t)dupk * MP + threadIdx.x];
+    }
+    __syncthreads();
   }
   if constexpr (GRAD) {
     if (threadIdx.x < d) {
@@ -1559,17 +1582,21 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   }
   // One pair per wave, written as a one-shot block: nothing pair-invariant (psi's coefficients, lane
   // addresses) is hoisted out of a loop and kept live in registers.
-  double sv[M], mx0[M], ysd[M], ymu[M], nz[M], os[M];
+  // sv / mx0: the candidate's noiseless variance and mean (the slopes' normaliser, the gradient);
+  // l0v / l0m: what line 0 is built from (the same unless x_b coincides with a discretisation point)
+  double sv[M], mx0[M], ysd[M], ymu[M], nz[M], os[M], l0m[M], l0v[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const bool live = i < m;
     // workgroup-uniform: kept in SGPRs across the pair loop
-    ysd[i] = sgpr_f64(live ? s_pp[i * 6 + 0] : 1.0);
-    ymu[i] = sgpr_f64(live ? s_pp[i * 6 + 1] : 0.0);
-    nz[i] = sgpr_f64(live ? s_pp[i * 6 + 2] : 0.0);
-    os[i] = sgpr_f64(live ? s_pp[i * 6 + 3] : 0.0);
-    sv[i] = sgpr_f64(live ? s_pp[i * 6 + 4] : 0.0);
-    mx0[i] = sgpr_f64(live ? s_pp[i * 6 + 5] : 0.0);
+    ysd[i] = sgpr_f64(live ? s_pp[i * NPP + 0] : 1.0);
+    ymu[i] = sgpr_f64(live ? s_pp[i * NPP + 1] : 0.0);
+    nz[i] = sgpr_f64(live ? s_pp[i * NPP + 2] : 0.0);
+    os[i] = sgpr_f64(live ? s_pp[i * NPP + 3] : 0.0);
+    sv[i] = sgpr_f64(live ? s_pp[i * NPP + 4] : 0.0);
+    mx0[i] = sgpr_f64(live ? s_pp[i * NPP + 5] : 0.0);
+    l0m[i] = sgpr_f64(live ? s_pp[i * NPP + 6] : 0.0);
+    l0v[i] = sgpr_f64(live ? s_pp[i * NPP + 7] : 0.0);
   }
 
   // ---- staged streaming forward: the extremes pass and the filter pass of every pair of the workgroup
@@ -1595,8 +1622,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     double bb0 = 0.0, a0 = a_off, wbt = 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      bb0 = fma(wb[i], sv[i], bb0);
-      a0 = fma(wa[i], mx0[i], a0);
+      bb0 = fma(wb[i], l0v[i], bb0);
+      a0 = fma(wa[i], l0m[i], a0);
       wbt = (i == target) ? wb[i] : wbt;
     }
     const int nq = (NL + SCH - 1) / SCH;
@@ -1820,7 +1847,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     // is dead once the filter has run.
     double bb0 = 0.0;  // line 0's slope (the padding lines reuse it)
 #pragma unroll
-    for (int i = 0; i < M; ++i) bb0 = fma(wb[i], sv[i], bb0);
+    for (int i = 0; i < M; ++i) bb0 = fma(wb[i], l0v[i], bb0);
     // STREAM: chunk c of the lines straight from global memory
     auto build_chunk = [&](int c, double (&la)[MAXL], double (&lb)[MAXL]) {
       const int kbase = c * 64 * MAXL;
@@ -1849,7 +1876,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
       if (c == 0) {
         double a = a_off;  // line 0: the candidate itself (discretekg.py:182-183)
 #pragma unroll
-        for (int i = 0; i < M; ++i) a = fma(wa[i], mx0[i], a);
+        for (int i = 0; i < M; ++i) a = fma(wa[i], l0m[i], a);
         la[0] = (lane == 0) ? a : la[0];
         lb[0] = (lane == 0) ? bb0 : lb[0];
       }
@@ -1895,8 +1922,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
         double a = a_off, bb = 0.0;  // line 0: the candidate itself (discretekg.py:182-183)
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          a = fma(wa[i], mx0[i], a);
-          bb = fma(wb[i], sv[i], bb);
+          a = fma(wa[i], l0m[i], a);
+          bb = fma(wb[i], l0v[i], bb);
         }
         la[0] = (lane == 0) ? a : la[0];
         lb[0] = (lane == 0) ? bb : lb[0];
@@ -2171,7 +2198,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
         // - sum_e Dw_e b_e * dV/(2V), - [line 0 attains max a] da_0/dx
         double a0 = a_off;
 #pragma unroll
-        for (int i = 0; i < M; ++i) a0 = fma(wa[i], mx0[i], a0);
+        for (int i = 0; i < M; ++i) a0 = fma(wa[i], l0m[i], a0);
         const double tfac = (a0 == f.aT) ? 1.0 / (double)f.cntT : 0.0;
         if (lane == 0)
           for (int dd = 0; dd < d; ++dd) gw[48 + dd] += gw[dd] - sumDb * gw[32 + dd] - tfac * gw[16 + dd];
@@ -2232,8 +2259,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
           double a = a_off, bb = 0.0;  // line 0: the candidate itself (discretekg.py:182-183)
 #pragma unroll
           for (int i = 0; i < M; ++i) {
-            a = fma(wa[i], mx0[i], a);
-            bb = fma(wb[i], sv[i], bb);
+            a = fma(wa[i], l0m[i], a);
+            bb = fma(wb[i], l0v[i], bb);
           }
           lb[0] = (lane == 0) ? bb : lb[0];
           return a;
@@ -2256,8 +2283,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
           double a0 = a_off, b0 = 0.0;
 #pragma unroll
           for (int i = 0; i < M; ++i) {
-            a0 = fma(wa[i], mx0[i], a0);
-            b0 = fma(wb[i], sv[i], b0);
+            a0 = fma(wa[i], l0m[i], a0);
+            b0 = fma(wb[i], l0v[i], b0);
           }
           const double A1 = P->itop[j];
           const int k1 = P->itopk[2 * j], c1 = P->itopk[2 * j + 1];
@@ -2314,68 +2341,87 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
 #ifndef DKG_STG_STAMPS
   if (!GRAD) KST(st, 5);
 #endif
-  // The candidate's KG is (sum of its S pair values in pair order) / S, and dKG/dx likewise, whatever the
-  // launch geometry (waves per workgroup, workgroups per candidate; envelope_geometry): one workgroup sums
-  // its pairs itself; with several, every workgroup leaves its pairs' values in the plan's per-pair slots
-  // and the last to arrive (ticket) sums all S in order, so a narrow small-batch launch, the fused launch
-  // and the wide launch give the same bits.  The last workgroup re-zeroes the ticket for the next launch.
-  __shared__ int s_lastk;  // G > 1: this workgroup arrived last for its candidate (kg's ticket)
-  if constexpr (GRAD) {
-    if (threadIdx.x < d) {
-      if (G == 1) {
-        double gs = 0.0;
-        for (int w2 = 0; w2 < SW; ++w2) gs += sgw[w2 * 64 + 48 + threadIdx.x];
-        gs /= (double)S;
-        dkg[(size_t)b * d + threadIdx.x] = gs;
-        if (hout != nullptr) hout[(size_t)B + (size_t)b * d + threadIdx.x] = gs;
-      } else {
-        for (int q = 0; q < j1 - j0; ++q)
-          P->wg_gpart[((size_t)b * S + j0 + q) * d + threadIdx.x] = sgw[q * 64 + 48 + threadIdx.x];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      }
-    }
-    if (G > 1) __syncthreads();  // the partials are out before thread 0 takes the ticket
-  }
-  if (threadIdx.x == 0) {
-    if (G == 1) {
-      double s = 0.0;
-      for (int q = 0; q < j1 - j0; ++q) s += skg[q];
-      kg[b] = s / (double)S;
-      if constexpr (GRAD) {
-        if (hout != nullptr) hout[b] = kg[b];
-      }
+  // The candidate's KG, whatever the launch geometry (waves per workgroup, workgroups per candidate:
+  // envelope_geometry), is  sum_g G_g / S  over the groups g of 8 consecutive pairs, G_g the group's pair
+  // values summed in pair order, the groups folded in order; dKG/dx likewise.  So a narrow small-batch launch,
+  // the fused launch and the wide launch give the same bits:
+  //  * a workgroup of 8 waves holds a whole group and sums it from LDS; narrower workgroups (small batches)
+  //    leave their pair values in the plan (write-through stores, drained), count themselves into the
+  //    group's ticket, and the group's last arriver sums the 8 values in order (write-through loads: no
+  //    fence, cdna_hip_programming.md Guideline 16, every handed-off byte sc1);
+  //  * one group: the group's sum / S is the result; two groups: each adds its G_g / S onto the zeroed kg[b]
+  //    with one atomic (two addends onto 0 commute: the same bits in either order, and no workgroup waits);
+  //    more groups, or a pinned host copy to write: the group sums meet in the same ticket form, in order.
+  // The tickets and kg / dkg are zeroed by the cross stage of the launch sequence.
+  {
+    const int ng = (S + 7) >> 3;                 // groups of 8 pairs (a workgroup never spans two)
+    const int grp = j0 >> 3;
+    const int gpairs = min(8, S - 8 * grp);      // pairs in this workgroup's group
+    const int gwgs = (gpairs + SW - 1) / SW;     // workgroups sharing it (1 unless the launch is narrow)
+    const size_t prow = (size_t)b * (S + ng);    // wg_part row of candidate b: S pair values, ng group terms
+    int* tk = P->tickets + (size_t)b * (ng + 1); // [ng] group tickets, [ng] the candidate's
+    __shared__ int s_last;
+    const int dg = GRAD ? d : 0;
+    // ---- level 1: G_g (thread 0) and, GRAD, its gradient (threads 1 .. d, one coordinate each)
+    double gsum = 0.0;
+    const int gi = (int)threadIdx.x - 1;  // GRAD coordinate of this thread (threads 1 .. d)
+    if (gwgs == 1) {
+      if (threadIdx.x == 0)
+        for (int q = 0; q < j1 - j0; ++q) gsum += skg[q];
+      if (GRAD && gi >= 0 && gi < dg)
+        for (int q = 0; q < j1 - j0; ++q) gsum += sgw[q * 64 + 48 + gi];
     } else {
-      for (int q = 0; q < j1 - j0; ++q) P->wg_part[(size_t)b * S + j0 + q] = skg[q];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int prev = atomicAdd(&P->tickets[b], 1);
-      s_lastk = prev == G - 1;
-      if (prev == G - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        double tot = 0.0;
-        for (int q = 0; q < S; ++q)
-          tot += __hip_atomic_load(&P->wg_part[(size_t)b * S + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        kg[b] = tot / (double)S;
-        __hip_atomic_store(&P->tickets[b], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if constexpr (GRAD) {
-          if (hout != nullptr) hout[b] = kg[b];
-        }
+      if (threadIdx.x == 0)
+        for (int q = 0; q < j1 - j0; ++q) __hip_atomic_store(&P->wg_part[prow + j0 + q], skg[q], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+      if (GRAD && gi >= 0 && gi < dg)
+        for (int q = 0; q < j1 - j0; ++q)
+          __hip_atomic_store(&P->wg_gpart[(prow + j0 + q) * dg + gi], sgw[q * 64 + 48 + gi], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+      __syncthreads();
+      if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(&tk[grp], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gwgs - 1;
+      __syncthreads();
+      if (s_last) {
+        if (threadIdx.x == 0)
+          for (int q = 8 * grp; q < 8 * grp + gpairs; ++q)
+            gsum += __hip_atomic_load(&P->wg_part[prow + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (GRAD && gi >= 0 && gi < dg)
+          for (int q = 8 * grp; q < 8 * grp + gpairs; ++q)
+            gsum += __hip_atomic_load(&P->wg_gpart[(prow + q) * dg + gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-  }
-  if constexpr (GRAD) {
-    if (G > 1) {
+    const bool holds = (gwgs == 1 || s_last) && (threadIdx.x == 0 || (GRAD && gi >= 0 && gi < dg));
+    const double term = gsum / (double)S;
+    // where this thread's result goes: kg[b] (thread 0) or dkg[b][gi]; the host copy at the same offsets
+    double* dst_dev = threadIdx.x == 0 ? &kg[b] : (GRAD ? &dkg[(size_t)b * d + max(gi, 0)] : &kg[b]);
+    const size_t hoff = threadIdx.x == 0 ? (size_t)b : (size_t)B + (size_t)b * d + max(gi, 0);
+    // ---- level 2
+    const bool fold = ng > 2 || (hout != nullptr && ng > 1);
+    if (ng == 1) {
+      if (holds) {
+        *dst_dev = term;
+        if (hout != nullptr) hout[hoff] = term;
+      }
+    } else if (!fold) {
+      if (holds) atomicAdd(dst_dev, term);
+    } else if (gwgs == 1 || s_last) {  // workgroup-uniform
+      if (holds)
+        __hip_atomic_store(threadIdx.x == 0 ? &P->wg_part[prow + S + grp] : &P->wg_gpart[(prow + S + grp) * dg + gi],
+                           term, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (s_lastk && threadIdx.x < d) {  // the last workgroup: the gradient's per-pair partials in pair order
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(&tk[ng], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+      __syncthreads();
+      if (s_last && holds) {
         double tot = 0.0;
-        for (int q = 0; q < S; ++q)
-          tot += __hip_atomic_load(&P->wg_gpart[((size_t)b * S + q) * d + threadIdx.x], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        tot /= (double)S;
-        dkg[(size_t)b * d + threadIdx.x] = tot;
-        if (hout != nullptr) hout[(size_t)B + (size_t)b * d + threadIdx.x] = tot;
+        for (int q = 0; q < ng; ++q)
+          tot += __hip_atomic_load(threadIdx.x == 0 ? &P->wg_part[prow + S + q] : &P->wg_gpart[(prow + S + q) * dg + gi],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *dst_dev = tot;
+        if (hout != nullptr) hout[hoff] = tot;
       }
     }
   }
@@ -2408,7 +2454,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ cov_all,
                                                        const double* __restrict__ var_all,
                                                        const double* __restrict__ mux_all,
-                                                       const double* __restrict__ wts, long long cov_stride,
+                                                       const double* __restrict__ wts,
+                                                       const int* __restrict__ dupv, long long cov_stride,
                                                        int bpad, double* __restrict__ hout, int split) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
@@ -2417,7 +2464,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   int b, g;
   if (!xcd_group(blockIdx.x, B, split, b, g)) return;
   envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
-                                       cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout);
+                                       dupv, cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout);
 }
 
 // The lines of every (candidate, scalarisation) pair of the plan's last
@@ -2430,6 +2477,7 @@ __global__ __launch_bounds__(256) void lines_export_kernel(const Plan* __restric
   const int m = P->m, N = P->N, S = P->S, target = P->target, bpad = P->bpad;
   const bool full = target < 0;
   double sv[M], mx0[M], ysd[M], ymu[M], nz[M];
+  const int dk = P->dup[b];  // line 0 from that record when x_b coincides with a discretisation point
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const bool live = i < m;
@@ -2447,25 +2495,26 @@ __global__ __launch_bounds__(256) void lines_export_kernel(const Plan* __restric
   double* bo = b_out + ((size_t)b * S + j) * (N + 1);
   for (int k = threadIdx.x; k <= N; k += blockDim.x) {
     double a = a_off, bb = 0.0;
-    if (k == 0) {
+    if (k == 0 && dk == DUP_NONE) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         a = fma(wa[i], mx0[i], a);
         bb = fma(wb[i], sv[i], bb);
       }
     } else {
+      const int r = (k == 0) ? dk : k - 1;  // the record line k is built from (line 0: the coincident one)
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         if (i < m) {
-          a = fma(wa[i], P->mu_all[(size_t)(k - 1) * cov_rec(M) + i], a);
-          if (full) bb = fma(wb[i], P->cov_all[(size_t)b * P->cov_stride + (size_t)(k - 1) * cov_rec(M) + i], bb);
+          a = fma(wa[i], P->mu_all[(size_t)r * cov_rec(M) + i], a);
+          if (full) bb = fma(wb[i], P->cov_all[(size_t)b * P->cov_stride + (size_t)r * cov_rec(M) + i], bb);
         }
       }
       if (!full) {
         double wbt = 0.0;
 #pragma unroll
         for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
-        bb = wbt * P->cov_all[(size_t)b * P->cov_stride + (size_t)(k - 1) * cov_rec(M) + target];
+        bb = wbt * P->cov_all[(size_t)b * P->cov_stride + (size_t)r * cov_rec(M) + target];
       }
     }
     ao[k] = a;
@@ -2493,7 +2542,7 @@ hipError_t launch_env_t(const EnvLaunch& a) {
   raise_lds_limit((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>, a.lds);
   const Plan& h = *a.host;
   hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
-                     a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights,
+                     a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights, h.dup,
                      (long long)h.cov_stride, h.bpad, a.hout, h.split);
   return hipGetLastError();
 }

@@ -42,6 +42,7 @@ struct FusedArgs {
   const double* var_all;
   const double* mux_all;
   const double* wts;
+  const int* dup;
   long long cov_stride;
   int bpad;
   Handoff ho;
@@ -70,9 +71,13 @@ forward_fused_kernel(FusedArgs a) {
       // covariance workgroups of output 0 in this row block -> cnt2 -> the envelope's wait), so every
       // zero store is visible before any envelope workgroup of these candidates adds to it
       const int r1 = std::min(a.B, 16 * (ti + 1));
+      const int nt = pair_groups(P->S) + 1;
+      for (int i = 16 * ti * nt + (int)threadIdx.x; i < r1 * nt; i += blockDim.x) st_out<true>(&P->tickets[i], 0);
       for (int i = 16 * ti + (int)threadIdx.x; i < r1; i += blockDim.x) {
         st_out<true>(&a.kg[i], 0.0);
-        st_out<true>(&P->tickets[i], 0);
+        // (the covariance workgroups of the other outputs do not wait for this one, but every output's
+        // workgroups mark the same coincidences, output 0's after this store: the mark survives)
+        st_out<true>(&P->dup[i], DUP_NONE);
       }
     }
     cross_root_impl<DM, false, double, true>(P->o[oi], P->d, a.xnew, a.B, P->q[oi], P->mux[oi], ti, grp, smem, st);
@@ -90,7 +95,7 @@ forward_fused_kernel(FusedArgs a) {
   }
   const int e = id - a.nC - a.nV;
   envelope_body<MAXL, M, false, false, true>(P, a.B, a.kg, nullptr, a.dst, nullptr, nullptr, a.mu_all, a.cov_all,
-                                             a.var_all, a.mux_all, a.wts, a.cov_stride, a.bpad, e / a.split,
+                                             a.var_all, a.mux_all, a.wts, a.dup, a.cov_stride, a.bpad, e / a.split,
                                              e % a.split, a.split, smem, kst_slot_wg(a.dst, P, 2, e), &a.ho);
 }
 

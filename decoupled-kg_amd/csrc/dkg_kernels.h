@@ -12,6 +12,11 @@ namespace dkg {
 // per-output 8-byte reads the compiler pairs into ds_read2st64_b64 (128 B/clk).
 __host__ __device__ constexpr int cov_rec(int m) { return m <= 1 ? 1 : m <= 2 ? 2 : m <= 4 ? 4 : 8; }
 
+// Groups of 8 scalarisation pairs: the envelope stage's fixed summation order (envelope_body).
+__host__ __device__ constexpr int pair_groups(int S) { return (S + 7) >> 3; }
+// Plan::dup: no discretisation point coincides with the candidate.
+constexpr int DUP_NONE = 0x7fffffff;
+
 // Stage ablations (empty cross / covariance / envelope launches selected by
 // DKG_DEBUG_COV_FLAGS 2 / 1 and DKG_DEBUG_ENV_FLAGS 2) exist only in builds
 // with -DDKG_ABLATIONS=1: the check is a dependent scalar load at kernel entry.
@@ -67,9 +72,14 @@ struct Plan {
   double* cov_all;                  // [max_B][N][cov_rec(m)] posterior covariance rows, line records (workspace)
   double* mu_all;                   // [N][cov_rec(m)] the outputs' disc_mean, line records
   int64_t cov_stride;               // N * cov_rec(m): doubles per candidate in cov_all
-  double* wg_part;                  // [B x S] per-pair KG for the ordered sum over S (split > 1 only)
-  int* tickets;                     // [B] arrival counters (split > 1; the last workgroup re-zeroes its own)
-  double* wg_gpart;                 // GRAD: [B x S x d] per-pair dKG/dx for the ordered sum (split > 1 only)
+  double* wg_part;                  // [B][S + ng] pair values, then group terms (ng = ceil(S / 8); split > 1 only)
+  int* tickets;                     // [B][ng + 1] group and candidate arrival counters (zeroed by the cross stage)
+  // [B]: the lowest record k with z_k == x_b exactly (DUP_NONE: none), from the covariance stage (r^2 = 0).
+  // The reference's joint posterior over [x_b; D] makes line 0 and line k + 1 exact copies there (same rows
+  // of one covariance matrix), and the walk then takes line 0 (lowest index) while torch.max splits the
+  // gradient of max a between them; the envelope builds line 0 from record k so it is the same copy.
+  int* dup;
+  double* wg_gpart;                 // GRAD: [B][S + ng][d] as wg_part, for dKG/dx (split > 1 only)
   float* q32[DKG_MAX_OUTPUTS];      // F32: quad-packed K(x, X) R per output (workspace)
   float* root32[DKG_MAX_OUTPUTS];   // F32: quad-packed R^T (fp32 copy of root_frag, plan init)
   float* disc32[DKG_MAX_OUTPUTS];   // F32: quad-packed Q_D (fp32 copy of disc_frag, plan init)

@@ -181,7 +181,8 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a
 }
 
 // Forward: grid (B tiles, pairs, outputs); workgroup (0,0,0) also clears the
-// KG accumulators (and arrival tickets) the envelope stage adds into.
+// KG accumulators (and arrival tickets) the envelope stage adds into, and the
+// candidates' coincidence marks (Plan::dup) the covariance stage sets.
 template <int DM, class T = double>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const Plan* __restrict__ P,
                                                                           const double* __restrict__ xnew, int B,
@@ -193,8 +194,9 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const 
   if (blockIdx.x == 0 && blockIdx.y == 0 && oi == 0) {
     for (int i = threadIdx.x; i < B; i += blockDim.x) {
       kg[i] = 0.0;
-      P->tickets[i] = 0;
+      P->dup[i] = DUP_NONE;
     }
+    for (int i = threadIdx.x; i < B * (pair_groups(P->S) + 1); i += blockDim.x) P->tickets[i] = 0;
   }
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 2)) return;  // ablation: empty cross stage
   if constexpr (sizeof(T) == 8) {
@@ -240,11 +242,13 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_fwd_grad_kernel(const P
       for (int i = threadIdx.x; i < xa.n; i += blockDim.x) xstage[i] = xa.v[i];
   }
   if (z < m) {
-    if (blockIdx.x == 0 && blockIdx.y == 0 && z == 0)
+    if (blockIdx.x == 0 && blockIdx.y == 0 && z == 0) {
       for (int i = threadIdx.x; i < B; i += blockDim.x) {
         kg[i] = 0.0;
-        P->tickets[i] = 0;
+        P->dup[i] = DUP_NONE;
       }
+      for (int i = threadIdx.x; i < B * (pair_groups(P->S) + 1); i += blockDim.x) P->tickets[i] = 0;
+    }
     cross_root_impl<DM>(P->o[z], d, xnew, B, P->q[z], P->mux[z], blockIdx.x, blockIdx.y, smem, st, 0, nullptr,
                         P->qxrm[z]);
     return;
@@ -501,12 +505,12 @@ static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const doubl
 
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow) {
   // Up to 8 scalarisation waves of one candidate per workgroup, one pair per
-  // wave; with S <= 16 at most two workgroups per candidate, whose partial
-  // sums meet in one commutative atomic add (no inter-workgroup fences).
+  // wave; with S <= 16 at most two workgroups per candidate, whose group sums
+  // meet in one commutative atomic add (no inter-workgroup fences).
   // Small batches (narrow): fewer waves per workgroup until the launch has at least ENV_MIN_WGS
   // workgroups, so a B = 1 value+gradient call (the reference's optimize_acqf shape, batch_limit 1)
-  // spreads its S pairs over S CUs, one wave per SIMD, instead of two workgroups; more than two
-  // workgroups per candidate meet in the ordered per-workgroup partials (deterministic).
+  // spreads its S pairs over S CUs, one wave per SIMD, instead of two workgroups; the workgroups of
+  // one group of 8 pairs meet in ordered per-pair values (envelope_body: the same bits as the wide launch).
   constexpr int ENV_MIN_WGS = 128;
   int sw = std::max(1, std::min(8, S));
   if (narrow)
@@ -539,7 +543,7 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
     }
   }
   EnvLaunch a{&h, dev, B, kg, pairs, dim3(xcd_group_size(B, h.split)), dim3(h.sw * WAVE),
-              envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0, false, false), s, h.debug_stamp, nullptr,
+              envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0, false, !DKG_ICP), s, h.debug_stamp, nullptr,
               nullptr};
   return launch_env<false>(h, a);
 }
@@ -609,6 +613,7 @@ hipError_t launch_forward_auto(const Plan& h, const Plan* dev, const double* xne
   a.var_all = h.var_all;
   a.mux_all = h.mux_all;
   a.wts = h.weights;
+  a.dup = h.dup;
   a.cov_stride = (long long)h.cov_stride;
   a.bpad = h.bpad;
   // counters laid out for this B (every launch re-zeroes the range it used)

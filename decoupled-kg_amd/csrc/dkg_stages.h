@@ -460,6 +460,11 @@ __device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, c
     if (live && p0 < p1) load_batch(p0);
   }
   double kv[RV] = {};
+  // r^2 = 0: discretisation point k coincides with candidate b (Plan::dup).  The wave's hits are held as
+  // lane masks in SGPRs across the contraction (a per-lane mark took the kernel past 128 VGPRs) and
+  // marked with the stores (the fused launch: after its wait for the cross workgroups, one of which clears
+  // the marks of these candidates)
+  uint64_t hm[RV] = {};
   if (epi) {
     const double os = o.outputscale;
     const int kind = o.kernel;
@@ -479,6 +484,7 @@ __device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, c
         r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, disc_row(), o.inv_lengthscale, d);
       }
       kv[rr] = os * kernel_profile(kind, r2, EPI_FIRST ? tab : psi_tab());
+      hm[rr] = ballot(r2 == 0.0);
     }
   }
   if constexpr (HO) {
@@ -526,8 +532,10 @@ __device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, c
 #pragma unroll
       for (int q = 0; q < PC_KS - 1; ++q) sum += part[((q * NT + tt) * 4 + r) * 64 + lane];  // fixed order
       const int b = ti * 16 + mfma_drow<T>(lane, r);
-      if (b < B && k < N)  // line record k of candidate b, component oi (dkg_device.h cov_rec)
+      if (b < B && k < N) {  // line record k of candidate b, component oi (dkg_device.h cov_rec)
         st_out<HO>(&P->cov_all[(size_t)b * P->cov_stride + (size_t)k * cov_rec(P->m) + oi], kv[r] - sum);
+        if (hm[r] != 0 && ((hm[r] >> lane) & 1)) atomicMin(&P->dup[b], k);  // rare (wave-uniform test first)
+      }
     }
     if (want_var && lane < 16) {
       const int bb = ti * 16 + lane;
@@ -656,9 +664,12 @@ __global__ __launch_bounds__(PW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
         // K part 0 + K part 1 (fp addition commutes: the same bits whichever part adds)
         const double sum = acc[hr][hc][r] + part[(((hr * 4 + sb) * 2 + hc) * 4 + r) * 64 + lane];
         const int b = 16 * (ti0 + hr) + mfma_drow<double>(lane, r);
-        const double kv =
-            os * kernel_profile(kind, scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d));
-        if (b < B && k < N) P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kv - sum;
+        const double r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d);
+        const double kv = os * kernel_profile(kind, r2);
+        if (b < B && k < N) {
+          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kv - sum;
+          if (r2 == 0.0) atomicMin(&P->dup[b], k);  // Plan::dup
+        }
       }
     }
     if (want_var && lane < 16) {

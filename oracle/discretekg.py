@@ -126,6 +126,28 @@ def _kg_from_lines(intercepts: Tensor, slopes: Tensor) -> Tensor:
 
 
 # ---------------------------------------------------------------------------
+# Candidates on discretisation points.  The reference evaluates one joint posterior over [x; D]
+# (discretekg.py:182-184, 275-281): at x = z_k rows 0 and k + 1 of its covariance, and entries 0 and
+# k + 1 of its mean, are the same numbers in exact arithmetic, and identical bits whenever the BLAS
+# computes equal input rows identically (it does on this container's CPU; the GPU box's CPU BLAS was
+# seen not to, for one of nine grid points, profiles/r04/dup_probe.txt).  Line 0 and line k + 1 are then
+# exact copies: the walk takes line 0 (the lowest index among copies, :370-401) and torch.max splits the
+# gradient of max a between them (:225-233).  The restatement fixes that reading independently of BLAS
+# rounding: line 0 takes line k + 1's values (k the lowest coincident index) and keeps its own gradient.
+def coincident_index(xnew: Tensor, discretisation: Tensor):
+    """The lowest k with discretisation[k] == xnew exactly, or None."""
+    if discretisation.shape[0] == 0:
+        return None
+    hit = (discretisation == xnew.detach()).all(-1).nonzero()
+    return int(hit[0]) if hit.numel() else None
+
+
+def copy_row(v: Tensor, k: int) -> Tensor:
+    """v with entry 0 given entry k's value (its own gradient kept)."""
+    return torch.cat([(v[0] + (v[k] - v[0]).detach()).unsqueeze(0), v[1:]])
+
+
+# ---------------------------------------------------------------------------
 # discretekg.py:162-235
 def calculate_discrete_kg(model: ModelList, xnew: Tensor, discretisation: Tensor,
                           scalarisation_weights: Tensor) -> Tensor:
@@ -134,6 +156,9 @@ def calculate_discrete_kg(model: ModelList, xnew: Tensor, discretisation: Tensor
     Xt = torch.cat([xnew.unsqueeze(0), discretisation])
     post = model.posterior_list(Xt, observation_noise=False)            # :182-184
     post_noisy = model.posterior_list(xnew.unsqueeze(0), observation_noise=True)  # :185
+    kc = coincident_index(xnew, discretisation)
+    if kc is not None:  # line 0 an exact copy of line kc + 1 (see coincident_index)
+        post = [(copy_row(p[0], kc + 1), torch.cat([copy_row(p[1][0], kc + 1)[None], p[1][1:]])) for p in post]
     means = torch.stack([p[0] for p in post], dim=-1)                    # (N+1) x m
     S = scalarisation_weights.shape[0]
     kg = torch.zeros(S, dtype=scalarisation_weights.dtype)
@@ -161,6 +186,9 @@ def calculate_discrete_kg_conditioning_on_single_output(model: ModelList, xnew: 
     Xt = torch.cat([xnew.unsqueeze(0), discretisation])
     post = [m.posterior(Xt, observation_noise=False) for m in model.models]           # :275-281
     post_noisy = [m.posterior(xnew.unsqueeze(0), observation_noise=True) for m in model.models]  # :282-284
+    kc = coincident_index(xnew, discretisation)
+    if kc is not None:  # line 0 an exact copy of line kc + 1 (see coincident_index)
+        post = [(copy_row(p[0], kc + 1), torch.cat([copy_row(p[1][0], kc + 1)[None], p[1][1:]])) for p in post]
     means = torch.stack([p[0] for p in post], dim=-1)                    # :300
     cov_i = post[obj_idx_new][1][0]                                      # :301
     var_i = post_noisy[obj_idx_new][1][0, 0]                             # :302
@@ -248,6 +276,11 @@ def lines_batched(model: ModelList, X: Tensor, D: Tensor, W: Tensor, target=None
         var_noisy.append((v + om.noise) * om.y_std**2)
     mus = torch.stack(mus, -1)           # B x (N+1) x m
     covs = torch.stack(covs, -1)         # B x (N+1) x m
+    for bi in range(B):  # candidates on discretisation points: line 0 a copy of line k + 1 (coincident_index)
+        kc = coincident_index(X[bi], D)
+        if kc is not None:
+            mus = torch.cat([mus[:bi], copy_row(mus[bi], kc + 1)[None], mus[bi + 1:]])
+            covs = torch.cat([covs[:bi], copy_row(covs[bi], kc + 1)[None], covs[bi + 1:]])
     var_noisy = torch.stack(var_noisy, -1)  # B x m
     a = torch.einsum("bkm,sm->bsk", mus, W)
     if target is None:

@@ -82,21 +82,65 @@ def test_smoke_pipeline_writes_the_reference_catalog(tmp_path):
 
 
 @pytest.mark.parametrize("seed", [0, 1])
-def test_smoke_pipeline_matches_the_oracle_run(seed):
-    """The device SMOKE loop against the same loop on the CPU oracle (tests/smoke_oracle.py; decisions
-    committed in tests/golden/smoke_oracle.json by make_smoke_oracle.py): at every BO step of both runs the
-    same objective is chosen (decoupled), the candidate agrees within the optimiser's tolerance (L-BFGS-B
-    stops at a relative decrease of 2.2e-9: |dx| ~ sqrt(2 * 2.2e-9 / curvature) ~ 1e-4; two oracle runs
-    on different BLAS thread splits already differ by 1e-8) and the acquisition value within 1e-6 relative
-    plus the 1e-8 an x that far from the optimum can cost."""
+def test_smoke_pipeline_matches_the_oracle_run(seed, monkeypatch):
+    """The device SMOKE loop against the same loop on the CPU oracle (tests/smoke_oracle.py).
+
+    Every optimisation of the device run is redone on the oracle from the same state: the same surrogate,
+    scalarisations and target, the same starting points.  L-BFGS-B then reaches the same candidate within
+    1e-6 (measured: <= 2e-8, profiles/r04/smoke_probe0.txt) and the same acquisition value within 1e-8
+    relative (measured <= 3e-10).  The raw samples' KG values, which pick the starting points, agree within
+    the stated KG tolerance.
+
+    The first BO step of both modes also matches the oracle run committed in tests/golden/smoke_oracle.json
+    (make_smoke_oracle.py) at the optimiser's tolerance: L-BFGS-B stops at a relative decrease of 2.2e-9,
+    so |dx| ~ 1e-4.  Later steps are compared on the objective choice only.  The surrogates use noise 1e-8
+    (bo_loop.py:583-588), so their conditioning (~1e10 for the 1.8-lengthscale output) amplifies rounding
+    in the observed values.  A rounding-level change of the device posterior mean moves the second full
+    step's optimum by 5e-4 and its value by 1.5e-5 relative.  That sensitivity is in the problem, not in
+    the KG, so only the per-step comparison above is held tight."""
+    import dkg_amd.optim as optim
+    from dkg_amd.utils import make_torch_std_grid
+    from smoke_oracle import oracle_acq_factory
+
     want = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
                                        "smoke_oracle.json")))["seeds"][str(seed)]
     state, *_ = load_golden("lengthscales0")
+    calls, cur = [], {}
+    orig_acq, orig_gen, orig_init = optim.DiscreteKgOptimisationSpec._acq, optim.gen_candidates_scipy, \
+        optim._no_grad_values
+
+    def acq_hook(self, model, input_dim, W, target):
+        cur["oracle"] = oracle_acq_factory(
+            model, make_torch_std_grid(self.n_discretisation_points_per_axis, input_dim, {"dtype": torch.double}),
+            W, target)
+        return orig_acq(self, model, input_dim, W, target)
+
+    def init_hook(acq, X, chunk):
+        y = orig_init(acq, X, chunk)
+        with torch.no_grad():
+            ref = cur["oracle"](X).reshape(-1)
+        # the stated KG tolerance, its floor 64 eps max|a| taken at |a| <= 50 (the observations' scale)
+        assert bool((y.cpu() - ref).abs().le(1e-6 * ref.abs() + 1e-12).all()), (y, ref)
+        return y
+
+    def gen_hook(ic, acq, lb, ub, options=None):
+        c, v = orig_gen(ic, acq, lb, ub, options)
+        calls.append((ic.clone(), cur["oracle"], lb, ub, options, c.cpu(), v.cpu()))
+        return c, v
+
+    monkeypatch.setattr(optim.DiscreteKgOptimisationSpec, "_acq", acq_hook)
+    monkeypatch.setattr(optim, "_no_grad_values", init_hook)
+    monkeypatch.setattr(optim, "gen_candidates_scipy", gen_hook)
     got = run_smoke(GPProblem(state, device=DEV), HYPER, seed=seed)
+    # separate: 2 steps x 2 objectives x 2 restarts (batch_limit 1); full: 2 steps x 2 restarts
+    assert len(calls) == 12
+    for ic, oacq, lb, ub, options, c, v in calls:
+        c_o, v_o = orig_gen(ic, oacq, lb, ub, options)
+        assert (c - c_o).abs().max() <= 1e-6, (ic, c, c_o)
+        assert float((v - v_o).abs().max()) <= 1e-8 * float(v_o.abs().max()) + 1e-15, (v, v_o)
     for mode in ("separate", "full"):
         g, w = got[mode], want[mode]
         assert g["obj_index"] == w["obj_index"], mode
-        for x, xr in zip(g["x"], w["x"]):
-            assert x == pytest.approx(xr, abs=1e-4), (mode, x, xr)
-        assert g["acq"] == pytest.approx(w["acq"], rel=1e-6, abs=1e-8), mode
+        assert g["x"][0] == pytest.approx(w["x"][0], abs=1e-4), (mode, g["x"][0], w["x"][0])
+        assert g["acq"][0] == pytest.approx(w["acq"][0], rel=1e-6, abs=1e-8), mode
         assert all(a > 0 for a in g["acq"])

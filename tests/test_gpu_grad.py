@@ -206,3 +206,49 @@ def test_flat_early_out_matches_the_full_gradient_path(target):
     zero = kg_f == 0
     zero[:8] = False
     assert float(g[zero].abs().max()) <= 1e-250 and float(g_f[zero].abs().max()) <= 1e-250
+
+
+def _faithful_grad(om, X, D, W, target):
+    """The oracle's structure-faithful forward (oracle.discretekg.discrete_kg_forward: the reference's joint
+    posterior over [x; D] per candidate) with autograd: at x = z_k its lines 0 and k + 1 are exact copies."""
+    from oracle.discretekg import discrete_kg_forward
+
+    Xr = X.clone().unsqueeze(-2).requires_grad_(True)
+    kg = discrete_kg_forward(om, Xr, D, W, target)
+    (g,) = torch.autograd.grad(kg.sum(), Xr)
+    return kg.detach(), g.squeeze(-2)
+
+
+@pytest.mark.parametrize("case", ["small", "parity6d", "headline", "smoke_grid"])
+@pytest.mark.parametrize("target", [None, 0, 1])
+def test_candidates_on_discretisation_points(case, target):
+    """Candidates exactly on discretisation points (L-BFGS-B stops on box corners, and the reference's grids
+    hold them).  The reference's joint posterior over [x_b; D] makes line 0 and line k + 1 exact copies there
+    (rows 0 and k + 1 of one covariance matrix), so its walk takes line 0, the lowest index, and torch.max
+    splits the gradient of max a between the copies.  The device builds line 0 from record k (Plan::dup, set
+    by the covariance stage where r^2 = 0): KG (stated tolerance) and dKG/dx against the faithful oracle's
+    autograd, and line 0 equal to line k + 1 bit for bit in the exported lines."""
+    from dkg_amd.utils import make_torch_std_grid
+
+    if case == "smoke_grid":  # the SMOKE run's problem and 3 x 3 grid (bo_loop.py:122-131): every grid point
+        state, om, _, W, X, _ = load_golden("lengthscales0")
+        model = state
+        D = make_torch_std_grid(3, 2, {"dtype": torch.double})
+        idx = torch.arange(D.shape[0])
+        X = torch.cat([D, X[:3]])
+    else:
+        model, D, X, W = make_problem(WORKLOADS[case])
+        om = to_oracle(model)
+        idx = torch.linspace(0, D.shape[0] - 1, 9).round().long()
+        X = torch.cat([D[idx], X[:3]])
+    W = W[:8]
+    kg_ref, g_ref = _faithful_grad(om, X, D, W, target)
+    kg, g = native_grad(model, X, D, W, target)
+    amax = lines_batched(om, X, D, W, target)[0].abs().amax((-1, -2))
+    assert_within(kg, kg_ref, stated_tol(kg_ref, amax), "KG at discretisation points")
+    r = assert_grad_close(g, g_ref, grad_scale(om, X, D, W, target))
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    a, b = acq._plan_for(X.shape[0]).lines(X.to(DEV).contiguous())
+    for row, k in enumerate(idx.tolist()):
+        assert torch.equal(a[row, :, 0], a[row, :, k + 1]) and torch.equal(b[row, :, 0], b[row, :, k + 1]), row
+    print(f"{case} target={target}: gradient worst err/tol {r:.3g}")
