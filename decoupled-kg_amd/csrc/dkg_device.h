@@ -71,6 +71,11 @@ constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lin
 #ifndef DKG_ICP
 #define DKG_ICP 0
 #endif
+// The staged forward takes T (max a, tie: min b) from the plan's per-scalarisation top intercept when that
+// decides it (TopHint), instead of two wave reductions.
+#ifndef DKG_TOP_HINT
+#define DKG_TOP_HINT 1
+#endif
 // Streaming forward with LDS-staged chunks (M = 2..4): the extremes and filter passes read the line
 // records from LDS, STAGED_SLOTS * 64 lines per chunk, double-buffered and shared by the workgroup's pairs.
 constexpr int STAGED_SLOTS = 8;
@@ -1443,6 +1448,18 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   // candidate b's coincidence mark (the covariance stage's; loaded with the first batch, used after the wait)
   int dupk = DUP_NONE;
   if constexpr (!HO) dupk = dupv[b];
+  // this wave's scalarisation's top intercept over k >= 1 (TopHint), read with the first batch
+  double hA1 = 0.0;
+  int hk1 = 0, hc1 = 0;
+  constexpr bool HINT = DKG_TOP_HINT && !GRAD && !STREAM && !HO;
+  if constexpr (HINT) {
+    if (P->itop != nullptr) {
+      const int jh = min(g * SW + wave, S - 1);
+      hA1 = P->itop[jh];
+      hk1 = P->itopk[2 * jh];
+      hc1 = P->itopk[2 * jh + 1];
+    }
+  }
   if (threadIdx.x < m) {
 #pragma unroll
     for (int q = 0; q < (HO ? 4 : NPP); ++q) s_pp[threadIdx.x * NPP + q] = pp[q];
@@ -2229,6 +2246,44 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
                                     ? P->kstamps + ((size_t)b * S + j) * 8 : nullptr;
       // pairs_out also records the envelope size: every pair is walked then
       const bool flat_ok = pairs_out == nullptr && !force_walk;
+      // T without a wave reduction when the plan's top intercept decides it (TopHint): the intercepts of lines
+      // k >= 1 do not depend on the candidate, so the plan keeps each scalarisation's largest (Plan::itop)
+      TopHint hint{false, 0.0, 0.0};
+      if (HINT && flat_ok && P->itop != nullptr) {
+        double a0 = a_off, b0 = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          a0 = fma(wa[i], l0m[i], a0);
+          b0 = fma(wb[i], l0v[i], b0);
+        }
+        const double A1 = hA1;
+        const int k1 = hk1, c1 = hc1;
+        if (a0 > A1) {
+          hint = TopHint{true, a0, b0};
+        } else if (a0 < A1 && c1 == 1) {
+          // line k1's slope, as the build computes it (record k1 - 1)
+          const double* r = lcv + (size_t)(k1 - 1) * MP;
+          double bk = 0.0;
+          if (full) {
+            if constexpr (MP == 1) {
+              bk = fma(wb[0], r[0], bk);
+            } else {
+#pragma unroll
+              for (int q = 0; 2 * q < M; ++q) {
+                const double2 u = *reinterpret_cast<const double2*>(r + 2 * q);
+                bk = fma(wb[2 * q], u.x, bk);
+                if (2 * q + 1 < M) bk = fma(wb[2 * q + 1], u.y, bk);
+              }
+            }
+          } else {
+            double wbt = 0.0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
+            bk = wbt * r[target];
+          }
+          hint = TopHint{true, A1, bk};
+        }
+      }
       if constexpr (ICP) {
         // intercepts from the plan (first build: the registers loaded ahead; a rebuild: global memory)
         auto slopes = [&](double (&lb)[MAXL]) {
@@ -2277,49 +2332,13 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
           for (int t = 0; t < MAXL; ++t) la[t] = icp[lane + 64 * t];
           la[0] = (lane == 0) ? a0 : la[0];
         };
-        // T without a wave reduction when the plan's top intercept decides it (TopHint)
-        TopHint hint{false, 0.0, 0.0};
-        if (flat_ok) {
-          double a0 = a_off, b0 = 0.0;
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            a0 = fma(wa[i], l0m[i], a0);
-            b0 = fma(wb[i], l0v[i], b0);
-          }
-          const double A1 = P->itop[j];
-          const int k1 = P->itopk[2 * j], c1 = P->itopk[2 * j + 1];
-          if (a0 > A1) {
-            hint = TopHint{true, a0, b0};
-          } else if (a0 < A1 && c1 == 1) {
-            // line k1's slope, as the build computes it (record k1 - 1)
-            const double* r = lcv + (size_t)(k1 - 1) * MP;
-            double bk = 0.0;
-            if (full) {
-              if constexpr (MP == 1) {
-                bk = fma(wb[0], r[0], bk);
-              } else {
-#pragma unroll
-                for (int q = 0; 2 * q < M; ++q) {
-                  const double2 u = *reinterpret_cast<const double2*>(r + 2 * q);
-                  bk = fma(wb[2 * q], u.x, bk);
-                  if (2 * q + 1 < M) bk = fma(wb[2 * q + 1], u.y, bk);
-                }
-              }
-            } else {
-              double wbt = 0.0;
-#pragma unroll
-              for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
-              bk = wbt * r[target];
-            }
-            hint = TopHint{true, A1, bk};
-          }
-        }
         kgj = env_pair_regs<MAXL>(again, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst, flat_ok, &first, hint);
       } else {
         // the lines are rebuilt from the staged LDS data if the list walk cannot finish,
         // so no register line is live across it
         auto rebuild = [&](double (&la)[MAXL], double (&lb)[MAXL]) { build_lines(la, lb); };
-        kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst, flat_ok);
+        kgj = env_pair_regs<MAXL>(rebuild, NL, lane, sb, sa, sif, force_walk, &hn, nullptr, pst, flat_ok,
+                                  static_cast<const int*>(nullptr), hint);
       }
     }
     if (pairs_out != nullptr && lane == 0) {

@@ -68,30 +68,29 @@ __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __re
       for (int c = 0; c < LB; ++c) sL[lane][c] = (c <= lane) ? a[c] : 0.0;
     }
     if (lane == 0) bad = fail;
+    if (fail == 0) {
+      // W = L^{-1} by columns in the same wave: lane c solves L w = e_c, the entries L[j][q] reaching every lane
+      // by v_readlane from lane j (as in the factorisation: no LDS round trip; an LDS-broadcast form with the
+      // solution in registers took 256 VGPRs and 3.6 KB of scratch per lane)
+      double w[LB];
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        double acc = (lane == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int q = 0; q < j; ++q) acc = fma(-readlane_f64(a[q], j), w[q], acc);
+        w[j] = acc / readlane_f64(a[j], j);
+      }
+      if (lane < nb) {
+#pragma unroll
+        for (int r = 0; r < LB; ++r)
+          if (r < nb) X[(size_t)(k0 + r) * n + k0 + lane] = w[r];
+      }
+    }
   }
   __syncthreads();
   if (bad != 0) {
     if (tid == 0) *info = bad;
     return;
-  }
-  if (tid < LB) {
-    // W = L^{-1} by columns: thread c solves L w = e_c (forward substitution; the row of L it needs is the
-    // same for every thread: LDS broadcast reads)
-    const int c = tid;
-    double w[LB];
-#pragma unroll
-    for (int r = 0; r < LB; ++r) {
-      double acc = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int q = 0; q < r; ++q) acc = fma(-sL[r][q], w[q], acc);
-      w[r] = acc / sL[r][r];
-      asm volatile("" ::: "memory");  // one row of L live at a time (as in the row solves)
-    }
-    if (c < nb) {
-#pragma unroll
-      for (int r = 0; r < LB; ++r)
-        if (r < nb) X[(size_t)(k0 + r) * n + k0 + c] = w[r];
-    }
   }
   for (int e = tid; e < nb * nb; e += blockDim.x) {
     const int r = e / nb, c = e % nb;
