@@ -16,6 +16,12 @@
 namespace dkg {
 
 constexpr int LB = 32;  // block width
+#ifndef DKG_CHOL_TIMING
+#define DKG_CHOL_TIMING 0
+#endif
+#ifndef DKG_CHOL_LDS_BCAST
+#define DKG_CHOL_LDS_BCAST 1
+#endif
 
 // Lower tile (ti, tj), tj <= ti, of the row-major enumeration t = ti (ti + 1) / 2 + tj.
 __device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
@@ -33,8 +39,14 @@ __device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
 __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __restrict__ X, int n, int kb,
                                             int* __restrict__ info, double (*sC)[LB + 1], double (*sL)[LB + 1]) {
   __shared__ int bad;
+  __shared__ __attribute__((aligned(16))) double scol[2][LB];  // the factoring wave's current column (by parity)
+  __shared__ __attribute__((aligned(16))) double sT[16][17];    // W = L^{-1}: L21 W11
   const int k0 = kb * LB, nb = min(LB, n - k0);
   const int tid = threadIdx.x;
+#if DKG_CHOL_TIMING
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long t1 = 0;
+#endif
   if (tid < 64) {
     // one wave, lane r holds row r (rows past nb are identity rows); column j's pivot and entries reach
     // the other lanes by v_readlane, so the 32 steps need no LDS round trip and no barrier
@@ -51,8 +63,29 @@ __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __re
         if (!(piv > 0.0) || !isfinite(piv)) {  // NaN fails too
           fail = k0 + j + 1;
         } else {
-          const double dj = sqrt(piv);
-          a[j] = (lane == j) ? dj : ((lane > j) ? a[j] / dj : a[j]);
+          // 1/sqrt(piv) by v_rsq_f64 and one Newton step, then L[j][j] = piv / sqrt(piv) and L[c][j] = a / sqrt(piv)
+          // as products (the correctly rounded sqrt and division sequences made the step's dependent chain)
+          double rq = __builtin_amdgcn_rsq(piv);
+          rq = rq * fma(-0.5 * piv, rq * rq, 1.5);
+          const double dj = piv * rq;
+          // (entries above the diagonal take part unmasked: they are never read into the lower triangle, and the
+          // rows are masked when the factor leaves the registers)
+          a[j] = (lane == j) ? dj : a[j] * rq;
+#if DKG_CHOL_LDS_BCAST
+          // column j through LDS: one store, then every lane reads L[c][j] (c > j) back as broadcasts
+          // (16-byte reads of two entries) instead of 31 v_readlane pairs.  Two buffers by column parity: a
+          // wave's LDS operations complete in issue order, so neither the read-after-write of this column nor
+          // the next column's store needs a fence
+          double* sc = scol[j & 1];
+          if (lane < LB) sc[lane] = a[j];
+#pragma unroll
+          for (int c = j + 1; c < LB; ++c) {
+            if (c < nb) {
+              const double lcj = sc[c];  // L[c][j]
+              a[c] = fma(-a[j], lcj, a[c]);
+            }
+          }
+#else
 #pragma unroll
           for (int c = j + 1; c < LB; ++c) {
             if (c < nb) {
@@ -60,6 +93,7 @@ __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __re
               a[c] = (lane >= c) ? fma(-a[j], lcj, a[c]) : a[c];
             }
           }
+#endif
         }
       }
     }
@@ -68,26 +102,73 @@ __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __re
       for (int c = 0; c < LB; ++c) sL[lane][c] = (c <= lane) ? a[c] : 0.0;
     }
     if (lane == 0) bad = fail;
+#if DKG_CHOL_TIMING
+    t1 = __builtin_amdgcn_s_memtime();
+#endif
     if (fail == 0) {
-      // W = L^{-1} by columns in the same wave: lane c solves L w = e_c, the entries L[j][q] reaching every lane
-      // by v_readlane from lane j (as in the factorisation: no LDS round trip; an LDS-broadcast form with the
-      // solution in registers took 256 VGPRs and 3.6 KB of scratch per lane)
-      double w[LB];
+      // W = L^{-1} as 2 x 2 blocks of 16: lanes 0-15 solve L11 w = e_c (W11's columns) while lanes 16-31 solve
+      // L22 w = e_c (W22's), 16 steps each, the entries L[j][q] read from sL as broadcasts within each half;
+      // then W21 = -W22 (L21 W11) by two 16 x 16 MFMA products (the single 32-step solve with v_readlane
+      // broadcasts took ~35 K cycles)
+      const int h = (lane >> 4) & 1, cc = lane & 15, base = 16 * h;
+      double w[16];
 #pragma unroll
-      for (int j = 0; j < LB; ++j) {
-        double acc = (lane == j) ? 1.0 : 0.0;
+      for (int j = 0; j < 16; ++j) {
+        double acc = (cc == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int q = 0; q < j; ++q) acc = fma(-readlane_f64(a[q], j), w[q], acc);
-        w[j] = acc / readlane_f64(a[j], j);
+        for (int q = 0; q < j; ++q) acc = fma(-sL[base + j][base + q], w[q], acc);
+        w[j] = acc / sL[base + j][base + j];
       }
-      if (lane < nb) {
+      __shared__ double sW11[16][17];
+      if (lane < 16) {
 #pragma unroll
-        for (int r = 0; r < LB; ++r)
-          if (r < nb) X[(size_t)(k0 + r) * n + k0 + lane] = w[r];
+        for (int j = 0; j < 16; ++j) sW11[j][cc] = w[j];
+      }
+      // T = L21 W11 (A: L21 from sL rows 16..31, cols 0..15; B: W11), then W21 = -(W22 T) (A: W22, B: T)
+      d4 t = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kb2 = 0; kb2 < 4; ++kb2) {
+        const int kk = 4 * kb2 + (lane >> 4);
+        t = mfma_f64(sL[16 + (lane & 15)][kk], sW11[kk][lane & 15], t);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sT[(lane >> 4) + 4 * r][lane & 15] = t[r];
+      double w22[16];  // lanes 16..31 hold W22's column cc; broadcast through LDS for the MFMA A operand
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w22[j] = w[j];
+      __shared__ double sW22[16][17];
+      if (h == 1 && lane < 32) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sW22[j][cc] = w22[j];
+      }
+      d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kb2 = 0; kb2 < 4; ++kb2) {
+        const int kk = 4 * kb2 + (lane >> 4);
+        u = mfma_f64(sW22[lane & 15][kk], sT[kk][lane & 15], u);
+      }
+      // X's diagonal block: W11 (top left), W21 (bottom left), W22 (bottom right), zeros at the top right (the
+      // panel solves and the inverse's MFMAs read the whole block)
+      if (lane < 32) {
+        const int c = lane;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int r = base + j;
+          if (r < nb && c < nb) X[(size_t)(k0 + r) * n + k0 + c] = (h == 0) ? w[j] : w22[j];
+          if (h == 1 && j < nb && c < nb) X[(size_t)(k0 + j) * n + k0 + c] = 0.0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 + (lane >> 4) + 4 * r, col = lane & 15;
+        if (row < nb && col < nb) X[(size_t)(k0 + row) * n + k0 + col] = -u[r];
       }
     }
   }
   __syncthreads();
+#if DKG_CHOL_TIMING
+  if (tid == 0) printf("chol kb %d factor %llu inverse %llu\n", kb, t1 - t0, __builtin_amdgcn_s_memtime() - t1);
+#endif
   if (bad != 0) {
     if (tid == 0) *info = bad;
     return;
@@ -111,6 +192,9 @@ __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __re
 // the panels to the lower triangle at the end.
 __global__ __launch_bounds__(256) void chol_step_kernel(PrepBatch bt, int kb) {
   __shared__ double sP[LB][LB + 1], sQ[LB][LB + 1], sW[LB][LB + 1];
+#if DKG_CHOL_TIMING
+  const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
+#endif
   const int o = blockIdx.y;
   const int n = bt.n[o];
   double* __restrict__ A = bt.A[o];
@@ -136,28 +220,43 @@ __global__ __launch_bounds__(256) void chol_step_kernel(PrepBatch bt, int kb) {
   lower_tile(blockIdx.x, ti, tj);
   const int bi = kb + 1 + ti, bj = kb + 1 + tj;
   const int k0 = kb * LB, i0 = bi * LB, j0 = bj * LB;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int si = wave >> 1, sj = wave & 1;  // this wave's 16 x 16 sub-tile
+  // every global operand of the workgroup in flight at once, before the first barrier: the panels' A_ik /
+  // A_jk entries this lane feeds its MFMAs, the A_ij entries it updates, and W_kk into LDS
+  double pa[LB / 4], qa[LB / 4], aij[4];
+  {
+    const int ra = i0 + 16 * si + (lane & 15), rb = j0 + 16 * si + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < LB / 4; ++q) {
+      const int kk = 4 * q + (lane >> 4);
+      pa[q] = (ra < n && k0 + kk < n) ? A[(size_t)ra * n + k0 + kk] : 0.0;
+      qa[q] = (bi != bj && rb < n && k0 + kk < n) ? A[(size_t)rb * n + k0 + kk] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * si + (lane >> 4) + 4 * r, col = 16 * sj + (lane & 15);
+      aij[r] = (i0 + row < n && j0 + col < n) ? A[(size_t)(i0 + row) * n + j0 + col] : 0.0;
+    }
+  }
   for (int e = tid; e < LB * LB; e += blockDim.x) {
     const int r = e / LB, c = e % LB;
     sW[r][c] = (k0 + r < n && k0 + c < n) ? X[(size_t)(k0 + r) * n + k0 + c] : 0.0;
   }
   __syncthreads();
-  const int lane = tid & 63, wave = tid >> 6;
-  const int si = wave >> 1, sj = wave & 1;  // this wave's 16 x 16 sub-tile
   // solved panel tile: dst[r][c] = sum_q A[r0 + r][k0 + q] W[c][q]
-  auto panel = [&](int r0, double (*dst)[LB + 1]) {
+  auto panel = [&](const double (&av)[LB / 4], double (*dst)[LB + 1]) {
     d4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int ra = r0 + 16 * si + (lane & 15);
 #pragma unroll
     for (int q = 0; q < LB / 4; ++q) {
       const int kk = 4 * q + (lane >> 4);
-      const double a = (ra < n && k0 + kk < n) ? A[(size_t)ra * n + k0 + kk] : 0.0;
-      acc = mfma_f64(a, sW[16 * sj + (lane & 15)][kk], acc);
+      acc = mfma_f64(av[q], sW[16 * sj + (lane & 15)][kk], acc);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) dst[16 * si + (lane >> 4) + 4 * r][16 * sj + (lane & 15)] = acc[r];
   };
-  panel(i0, sP);
-  if (bi != bj) panel(j0, sQ);
+  panel(pa, sP);
+  if (bi != bj) panel(qa, sQ);
   __syncthreads();
   double(*Q)[LB + 1] = (bi == bj) ? sP : sQ;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -171,7 +270,7 @@ __global__ __launch_bounds__(256) void chol_step_kernel(PrepBatch bt, int kb) {
   for (int r = 0; r < 4; ++r) {
     const int row = 16 * si + (lane >> 4) + 4 * r, col = 16 * sj + (lane & 15);
     const bool in = i0 + row < n && j0 + col < n;
-    const double v = in ? A[(size_t)(i0 + row) * n + j0 + col] - acc[r] : 0.0;
+    const double v = in ? aij[r] - acc[r] : 0.0;
     if (diag_next) sW[row][col] = v;  // sW is free (read before the barrier above)
     else if (in) A[(size_t)(i0 + row) * n + j0 + col] = v;
   }
@@ -184,6 +283,9 @@ __global__ __launch_bounds__(256) void chol_step_kernel(PrepBatch bt, int kb) {
   }
   if (diag_next) {
     __syncthreads();
+#if DKG_CHOL_TIMING
+    if (tid == 0) printf("chol kb %d update %llu\n", kb, __builtin_amdgcn_s_memtime() - tk0);
+#endif
     factor_diag(A, X, n, bi, info, sW, sQ);
   }
 }
