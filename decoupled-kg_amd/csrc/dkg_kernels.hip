@@ -503,6 +503,12 @@ static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const doubl
                : launch_cross_cov_tt<DM, double>(h, dev, xnew, B, kg, s, stage);
 }
 
+// Narrow small-batch geometry: off (DKG_ENV_NARROW=0).  At B = 1 its 16 one-wave workgroups staged the lines
+// 16 times and met in per-group tickets: the value+gradient envelope took 16.6 us against 14.1 us for two
+// 8-wave workgroups (profiles/r04/b1).
+#ifndef DKG_ENV_NARROW
+#define DKG_ENV_NARROW 0
+#endif
 void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow) {
   // Up to 8 scalarisation waves of one candidate per workgroup, one pair per
   // wave; with S <= 16 at most two workgroups per candidate, whose group sums
@@ -513,7 +519,7 @@ void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow)
   // one group of 8 pairs meet in ordered per-pair values (envelope_body: the same bits as the wide launch).
   constexpr int ENV_MIN_WGS = 128;
   int sw = std::max(1, std::min(8, S));
-  if (narrow)
+  if (narrow && DKG_ENV_NARROW)
     while (sw > 1 && (long long)B * ((S + sw - 1) / sw) < ENV_MIN_WGS) sw = (sw + 1) / 2;
   *waves_per_wg = sw;
   *split = (S + sw - 1) / sw;
