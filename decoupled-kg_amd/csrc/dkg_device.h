@@ -63,6 +63,12 @@ __device__ __forceinline__ unsigned long long* kst_slot(int dst, const Plan* P, 
 // multiplication); the hull edges are collected one per lane and psi is
 // evaluated for all of them at once.
 constexpr int ENV_CAP = 128;
+#ifndef DKG_ENV_REFINE
+#define DKG_ENV_REFINE 1
+#endif
+#ifndef DKG_REFINE_OVERFLOW  // a list past ENV_CAP filtered against the chain of its entries
+#define DKG_REFINE_OVERFLOW 1
+#endif
 constexpr int HCAP = 128;  // GRAD: queued envelope lines per wave before their gradient terms are flushed
 constexpr int STREAM_CHUNK = 16;  // register slots per streamed chunk (1024 lines)
 // Staged forward: the intercepts from the plan's per-scalarisation cache (Plan::icpt) instead of the staged
@@ -354,12 +360,12 @@ __device__ __forceinline__ bool env_flat(const double (&la)[MAXL], const double 
 
 // The margin chord filter (EnvChords) over register lines into the list
 // (capacity CAP entries; the count goes on past it).
-template <int MAXL, int CAP>
-__device__ __forceinline__ int env_compact(const double (&la)[MAXL], const double (&lb)[MAXL], const EnvChords& ch,
-                                           int lane, double* sb, double* sa, int* si) {
+template <int MAXL, int CAP, class Chords = EnvChords>
+__device__ __forceinline__ int env_compact(const double (&la)[MAXL], const double (&lb)[MAXL], const Chords& ch,
+                                           int lane, double* sb, double* sa, int* si, int cnt0 = 0) {
   // the keep masks of a group of four slots first (independent compares, no
   // branch between them), then the group's writes (rarely any)
-  int cnt = 0;
+  int cnt = cnt0;
 #pragma unroll
   for (int t0 = 0; t0 < MAXL; t0 += 4) {
     uint64_t mk[4];
@@ -382,6 +388,144 @@ __device__ __forceinline__ int env_compact(const double (&la)[MAXL], const doubl
     }
   }
   return cnt;
+}
+
+// Lists longer than ENV_REFINE_MIN after the L-T-R filter are filtered again against a longer chain: one
+// quickhull round over the register lines puts V1 (the line farthest above the chord L-T) and V2 (farthest
+// above T-R) into the chain L, V1, T, V2, R, and a line is kept iff it lies within the EnvChords margin of
+// one of the four chords' extensions.  Any chain of lines of the set with increasing slopes lies below the
+// upper hull H over its slope range (H is concave), so a line failing every chord is at least the margin
+// below H there -- the argument of the L-T-R filter, and WALK_XGUARD's guard holds unchanged; rounding in the
+// choice of V1 / V2 only changes which lines of the set form the chain.  The successor table of the walk costs
+// ~ entries^2 / 64 divisions per lane (a 17-entry list: 6-7 K cycles in table<32> against 2-3 K for <= 8), and a
+// list past ENV_CAP took the walk over all lines (25-37 K cycles, headline_nd).
+constexpr int ENV_REFINE_MIN = 16;
+
+struct EnvChain {
+  double s[4], k[4];  // chord c: keep a line iff fma(-s_c, b, a) >= k_c (k_c = +inf: no chord)
+};
+
+__device__ __forceinline__ void chain_chord(double bP, double aP, double bQ, double aQ, double Wb, double rel,
+                                            double& s, double& k) {
+  const double db = bQ - bP;
+  s = (db > 0.0) ? (aQ - aP) / db : 0.0;
+  const double tau = rel * (fmax(fabs(aP), fabs(aQ)) + fabs(s) * (fmax(fabs(bP), fabs(bQ)) + Wb) + Wb);
+  k = (db > 0.0) ? fma(-s, bP, aP) - tau : INFINITY;
+}
+
+// Heights above the chords L-T (u1) and T-R (u2), scaled by the chord's db > 0 (the same argmax); -inf off
+// the chord's slope range (NaN padding lines too).
+struct ChainHeights {
+  double bL, aL, bT, aT, bR, aR, db1, da1, db2, da2;
+  __device__ __forceinline__ explicit ChainHeights(const FwdEnv& f)
+      : bL(f.bL), aL(f.aL), bT(f.bT), aT(f.aT), bR(f.bR), aR(f.aR), db1(f.bT - f.bL), da1(f.aT - f.aL),
+        db2(f.bR - f.bT), da2(f.aR - f.aT) {}
+  __device__ __forceinline__ double u1(double b, double a) const {
+    return (b > bL && b < bT) ? fma(a - aL, db1, -(b - bL) * da1) : -INFINITY;
+  }
+  __device__ __forceinline__ double u2(double b, double a) const {
+    return (b > bT && b < bR) ? fma(a - aT, db2, -(b - bT) * da2) : -INFINITY;
+  }
+};
+
+// The chords of the chain L, V1, T, V2, R (a chord with no line above it stays whole), wave-uniform in SGPRs.
+__device__ __forceinline__ EnvChain chain_of(const FwdEnv& f, bool v1, double b1v, double a1v, bool v2, double b2v,
+                                             double a2v, double rel = WALK_MARGIN) {
+  const double Wb = f.bR - f.bL;
+  if (!v1) { b1v = f.bT; a1v = f.aT; }
+  if (!v2) { b2v = f.bR; a2v = f.aR; }
+  EnvChain c;
+  chain_chord(f.bL, f.aL, b1v, a1v, Wb, rel, c.s[0], c.k[0]);  // L - V1 (L - T without V1)
+  chain_chord(b1v, a1v, f.bT, f.aT, Wb, rel, c.s[1], c.k[1]);  // V1 - T (none without V1: db = 0)
+  chain_chord(f.bT, f.aT, b2v, a2v, Wb, rel, c.s[2], c.k[2]);  // T - V2 (T - R without V2)
+  chain_chord(b2v, a2v, f.bR, f.aR, Wb, rel, c.s[3], c.k[3]);  // V2 - R (none without V2)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    c.s[i] = sgpr_f64(c.s[i]);
+    c.k[i] = sgpr_f64(c.k[i]);
+  }
+  return c;
+}
+
+// Half of a chain's chords: the lines with slope <= bT (upper: > bT) tested against two chords.
+struct HalfChords {
+  EnvChords ch;
+  double bT;
+  bool upper;
+};
+
+__device__ __forceinline__ uint64_t env_keep_mask(const HalfChords& c, double a, double b) {
+  return env_keep_mask(c.ch, a, b) & (c.upper ? ballot(b > c.bT) : ballot(b <= c.bT));
+}
+
+__device__ __forceinline__ bool chain_keep1(const EnvChain& c, double b, double a) {
+  return fma(-c.s[0], b, a) >= c.k[0] || fma(-c.s[1], b, a) >= c.k[1] || fma(-c.s[2], b, a) >= c.k[2] ||
+         fma(-c.s[3], b, a) >= c.k[3];
+}
+
+// The list (cnt entries, ENV_REFINE_MIN < cnt <= ENV_CAP, line-index order) filtered against the chain
+// L, V1, T, V2, R built from its own entries (every upper-hull line of the set is in it), compacted in place in
+// the same order.  Two entries per lane at most: a few registers, one reduction round.  Returns the new count.
+__device__ __forceinline__ int env_refine_list(int cnt, int lane, double* sb, double* sa, int* si, const FwdEnv& f,
+                                               EnvChain* chain_only = nullptr, double rel = WALK_MARGIN) {
+  const ChainHeights H(f);
+  double eb[2], ea[2];
+  int ek[2];
+  bool ev[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = lane + 64 * q;
+    ev[q] = e < cnt;
+    const int ee = min(e, cnt - 1);
+    eb[q] = ev[q] ? sb[ee] : __builtin_nan("");
+    ea[q] = ev[q] ? sa[ee] : __builtin_nan("");
+    ek[q] = si[ee];
+  }
+  double m1 = fmax(H.u1(eb[0], ea[0]), H.u1(eb[1], ea[1]));
+  double m2 = fmax(H.u2(eb[0], ea[0]), H.u2(eb[1], ea[1]));
+  DKG_BUTTERFLY_ROW({
+    m1 = fmax(m1, partner_f64<S_>(m1));
+    m2 = fmax(m2, partner_f64<S_>(m2));
+  })
+  m1 = combine_rows(m1, [](double p, double q) { return fmax(p, q); });
+  m2 = combine_rows(m2, [](double p, double q) { return fmax(p, q); });
+  // the first entry (list order) attaining each maximum
+  double b1v = 0.0, a1v = 0.0, b2v = 0.0, a2v = 0.0;
+  const bool v1 = m1 > 0.0, v2 = m2 > 0.0;
+  if (v1) {
+    const uint64_t k0 = ballot(H.u1(eb[0], ea[0]) == m1), k1 = ballot(H.u1(eb[1], ea[1]) == m1);
+    const int q = k0 ? 0 : 1, w = __builtin_ctzll(k0 ? k0 : k1);
+    b1v = readlane_f64(q ? eb[1] : eb[0], w);
+    a1v = readlane_f64(q ? ea[1] : ea[0], w);
+  }
+  if (v2) {
+    const uint64_t k0 = ballot(H.u2(eb[0], ea[0]) == m2), k1 = ballot(H.u2(eb[1], ea[1]) == m2);
+    const int q = k0 ? 0 : 1, w = __builtin_ctzll(k0 ? k0 : k1);
+    b2v = readlane_f64(q ? eb[1] : eb[0], w);
+    a2v = readlane_f64(q ? ea[1] : ea[0], w);
+  }
+  const EnvChain c = chain_of(f, v1, b1v, a1v, v2, b2v, a2v, rel);
+  if (chain_only != nullptr) {  // an overflowing list: the chain only (the caller filters the lines)
+    *chain_only = c;
+    return cnt;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // every entry read before the list is rewritten
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int n = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const bool keep = ev[q] && chain_keep1(c, eb[q], ea[q]);
+    const uint64_t mk = ballot(keep);
+    if (keep) {
+      const int pos = n + lanes_below(mk);
+      sb[pos] = eb[q];
+      sa[pos] = ea[q];
+      si[pos] = ek[q];
+    }
+    n += __popcll(mk);
+  }
+  return n;
 }
 
 // Short-circuit index (dkg_epigraph): the first line attaining max a
@@ -462,6 +606,34 @@ __device__ __forceinline__ EdgeSum env_pair_regs_edges(Build&& build, int nl, in
       pst[3] = __builtin_amdgcn_s_memtime();
       pst[6] = (unsigned long long)f.cnt;
     }
+  }
+  // opaque copies of the chain ends: no term of the first filter's chords is kept live for the later filters
+  asm volatile("" : "+v"(f.bL), "+v"(f.aL), "+v"(f.bT), "+v"(f.aT), "+v"(f.bR), "+v"(f.aR));
+  if (DKG_ENV_REFINE && f.cnt > ENV_REFINE_MIN && !force_walk) {  // wave-uniform: the chain L, V1, T, V2, R
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (f.cnt <= ENV_CAP) {
+      f.cnt = env_refine_list(f.cnt, lane, sb, sa, si, f);
+    } else if (DKG_REFINE_OVERFLOW) {
+      // the chain of the entries the list holds (lines of the set), then the lines filtered against it in
+      // two halves: slopes <= bT against the chords L-V1, V1-T, the rest against T-V2, V2-R (the largest
+      // height of a line above the chain is at the breakpoint its slope brackets), each half in line order
+      EnvChain c;
+      env_refine_list(ENV_CAP, lane, sb, sa, si, f, &c);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double la[MAXL], lb[MAXL];
+      build(la, lb);
+      const double bT = sgpr_f64(f.bT);
+      int n = env_compact<MAXL, ENV_CAP>(la, lb, HalfChords{{c.s[0], c.k[0], c.s[1], c.k[1]}, bT, false}, lane, sb,
+                                         sa, si);
+      n = env_compact<MAXL, ENV_CAP>(la, lb, HalfChords{{c.s[2], c.k[2], c.s[3], c.k[3]}, bT, true}, lane, sb, sa,
+                                     si, n);
+      f.cnt = n;
+    }
+    if (pst) pst[6] |= (unsigned long long)min(f.cnt, 0xffff) << 16;
   }
   if (!force_walk) {
     // up to three list walks: at WALK_MARGIN; after an overflow at the tight margin; after a
@@ -2242,7 +2414,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     } else if constexpr (STREAM) {
       kgj = env_pair_stream<MAXL>(nch, NL, lane, sb, sa, sif, vreg, force_walk, &hn, build_chunk);
     } else {
-      unsigned long long* pst = (dst == 2 && lane == 0 && (size_t)b * S + j < 2 * KST_WG)
+      // wave-uniform (every lane writes the same stamps): a pointer that stays in SGPRs
+      unsigned long long* pst = (dst == 2 && (size_t)b * S + j < 2 * KST_WG)
                                     ? P->kstamps + ((size_t)b * S + j) * 8 : nullptr;
       // pairs_out also records the envelope size: every pair is walked then
       const bool flat_ok = pairs_out == nullptr && !force_walk;

@@ -48,7 +48,12 @@ full = (s[:, 7] >> 32) & 1
 refilt = (s[:, 7] >> 33) & 1
 flat = ((s[:, 7] >> 34) & 1).astype(bool)
 hull = s[:, 7] & 0xffffffff
-cnt = s[:, 6]
+# pst[6]: the L-T-R list count (bits 0-15), after the chain refinement (16-31, 0: not refined), after the
+# last re-filter of the walk loop (32-47, 0: none)
+cnt0 = s[:, 6] & 0xffff
+cnt1 = (s[:, 6] >> 16) & 0xffff
+cnt2 = (s[:, 6] >> 32) & 0xffff
+cnt = np.where(cnt2 > 0, cnt2, np.where(cnt1 > 0, cnt1, cnt0))
 
 
 def q(v):
@@ -60,13 +65,14 @@ def q(v):
 
 print(f"pairs {P}, with stamps {ok.sum()} (the rest short-circuited)")
 print(f"flat (KG = 0 without a walk): {int(flat.sum())} pairs, compact/test {q(comp[flat])}")
-build, ext, comp, walked, walk, full, refilt, hull, cnt = (v[~flat] for v in (build, ext, comp, walked, walk, full, refilt, hull, cnt))
+build, ext, comp, walked, walk, full, refilt, hull, cnt, cnt0 = (
+    v[~flat] for v in (build, ext, comp, walked, walk, full, refilt, hull, cnt, cnt0))
 print("walked pairs:")
 print("build   ", q(build))
 print("extremes", q(ext))
 print("compact ", q(comp))
 print("walk    ", q(walk[walked]))
-print("list cnt", q(cnt))
+print("list cnt", q(cnt), " (L-T-R filter:", q(cnt0) + ")")
 print("hull    ", q(hull), " full-walk pairs", int(full.sum()), " refiltered pairs", int(refilt.sum()))
 print("list cnt hist", np.bincount(np.minimum(cnt, 130)).nonzero()[0][:40].tolist())
 for lo, hi in [(0, 8), (8, 16), (16, 32), (32, 64), (64, 129), (129, 10**9)]:
@@ -81,4 +87,4 @@ print("slowest pairs: total / build / extremes / compact / walk cycles, list, hu
 for r in order:
     w_ = (s[r, 5] - s[r, 3]) if s[r, 5] > s[r, 3] else (s[r, 4] - s[r, 3] if s[r, 4] > s[r, 3] else 0)
     print(f"  {tot[r]:6d} {s[r, 1] - s[r, 0]:6d} {s[r, 2] - s[r, 1]:6d} {s[r, 3] - s[r, 2]:6d} {w_:6d}"
-          f"  cnt {s[r, 6]:4d} hull {s[r, 7] & 0xffffffff:3d} flags {s[r, 7] >> 32:#x}")
+          f"  cnt {s[r, 6] & 0xffff:4d}/{(s[r, 6] >> 16) & 0xffff:3d}/{(s[r, 6] >> 32) & 0xffff:3d} hull {s[r, 7] & 0xffffffff:3d} flags {s[r, 7] >> 32:#x}")
