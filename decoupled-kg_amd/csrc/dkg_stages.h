@@ -6,6 +6,10 @@
 
 #include "dkg_device.h"
 
+#ifndef DKG_DUP_MARK  // A/B only: 0 drops the coincidence marks of the staged covariance (Plan::dup)
+#define DKG_DUP_MARK 1
+#endif
+
 namespace dkg {
 
 // Element-type plumbing of the two contractions (T = double: the reference's
@@ -484,7 +488,7 @@ __device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, c
         r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, disc_row(), o.inv_lengthscale, d);
       }
       kv[rr] = os * kernel_profile(kind, r2, EPI_FIRST ? tab : psi_tab());
-      hm[rr] = ballot(r2 == 0.0);
+      if (DKG_DUP_MARK) hm[rr] = ballot(r2 == 0.0);
     }
   }
   if constexpr (HO) {
