@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes (tools/pmc_passes.sh) for each benched workload, aggregated into profiles/r03/pmc_<workload>.json.
+# PMC passes (tools/pmc_passes.sh) for each benched workload, aggregated into <out>/pmc_<workload>.json (copied into profiles/r04/).
 set -uo pipefail
 out=${1:-gpurun_out/pmc}
 for wl in headline headline_nd stress; do

@@ -1,6 +1,6 @@
 """Worst parity ratios of the HIP forward against the oracle (GPU box, repo root).
 
-usage: python tools/parity_report.py [out.json]   (default profiles/r03_parity.json)
+usage: python tools/parity_report.py [out.json]   (default profiles/r04_parity.json)
 
 For every workload and path, tests/helpers.parity_case on the same candidates the GPU parity
 tests use: the device lines against oracle.lines_batched (relative gap), the envelope kernel on
@@ -23,7 +23,7 @@ CASES = [("small", 32), ("parity6d", 32), ("headline", 128), ("headline_nd", 128
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r03_parity.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04_parity.json")
     rep = {"line_rtol": LINE_RTOL, "cases": []}
     for wname, nX in CASES:
         model, D, X, W = make_problem(WORKLOADS[wname])
