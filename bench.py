@@ -58,7 +58,7 @@ FP64_VALU_MEASURED_TFLOPS = 61.4
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 SIMDS, CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMDs
-PMC_DIR = os.path.join(REPO, "profiles", "r03")
+PMC_DIR = os.path.join(REPO, "profiles", "r04")
 
 
 def parse():
@@ -95,7 +95,7 @@ def parse():
                     help="timed steps of the non-degenerate headline-size leg (workload headline_nd; 0 = skip)")
     ap.add_argument("--pmc", default="auto",
                     help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py); auto: "
-                         "profiles/r03/pmc_<workload>[_fp32].json, none if that file does not exist")
+                         "profiles/r04/pmc_<workload>[_fp32].json, none if that file does not exist")
     ap.add_argument("--prep-reps", type=int, default=5, help="timed device-state preparations (0 = skip)")
     ap.add_argument("--stress-steps", type=int, default=8,
                     help="timed forwards of the stress leg (BASELINE configs[4] shape, fp64; 0 = skip)")
@@ -365,6 +365,34 @@ class Throughput:
         if graphs and graph == 2 and launcher is not None:
             launcher.arm(0.0)
             launcher.close()
+        self.breakdown = None
+        if graphs and graph == 2 and launcher is None and steps == E:
+            # where a one-period region's time goes: the same launches again, untimed, with an event on every
+            # stream after each of its pieces (the head forward(s), then the rest) and the host clock after each
+            # hipGraphLaunch; GPU times relative to an event on the main stream just before the first launch
+            torch.cuda.synchronize()
+            e_start = torch.cuda.Event(enable_timing=True)
+            marks = [[torch.cuda.Event(enable_timing=True) for _ in range(npieces)] for _ in range(ns)]
+            e_start.record(streams[0])
+            launch_us = []
+            th0 = time.perf_counter()
+            for p in range(npieces):
+                for i, pieces in enumerate(execs[0]):
+                    if p < len(pieces):
+                        hip_check(hip.hipGraphLaunch(pieces[p], sptrs[i]), "hipGraphLaunch")
+                        launch_us.append(round((time.perf_counter() - th0) * 1e6, 1))
+                        marks[i][p].record(streams[i])
+            torch.cuda.synchronize()
+            wall_us = (time.perf_counter() - th0) * 1e6
+            done = [[round(e_start.elapsed_time(marks[i][p]) * 1e3, 1) for p in range(npieces)
+                     if p < len(execs[0][i])] for i in range(ns)]
+            self.breakdown = {
+                "what": "an untimed replay of the timed region's launches (steps == E: one period), per stream "
+                        "the GPU time at which each piece (its first `head` forwards, then the rest) had finished, "
+                        "and the host time after each hipGraphLaunch, both from just before the first launch",
+                "forwards_per_stream": [len(range(i, E, ns)) for i in range(ns)],
+                "host_launch_done_us": launch_us, "stream_piece_done_us": done,
+                "last_stream_done_us": max(d[-1] for d in done), "wall_us": round(wall_us, 1)}
         # this rank's device time of the forwards, and what the last exchange adds after them (exposed)
         self.compute_ms = ev0.elapsed_time(evc)
         self.exposed_ms = evc.elapsed_time(ev1)
@@ -632,7 +660,7 @@ def main():
         ws, ms, Ds, _, _, _, tps = setup("stress")
         es = tps.run(1, args.stress_steps, 2, False, world)
         fb = stage_model(ws, ws.m, [mm.num_train for mm in ms.models], Ds.shape[0], ws.B, ws.S, ws.d)
-        # the stress workload's own PMC file (profiles/r03/pmc_stress.json) for its stages' traffic / busy figures
+        # the stress workload's own PMC file (profiles/r04/pmc_stress.json) for its stages' traffic / busy figures
         pmc_s_path = os.path.join(PMC_DIR, "pmc_stress.json")
         pmc_s = json.load(open(pmc_s_path)) if os.path.exists(pmc_s_path) else {}
         st_s = stage_rooflines(tps.plan, tps.Xd, fb, 3, "fp64", pmc_s)
@@ -680,6 +708,7 @@ def main():
                        + (f", enqueued by {max(1, args.streams) if args.launch_threads < 0 else args.launch_threads}"
                           " host thread(s) side by side (dkg_launcher)" if args.graph == 2 else "")},
             "host_launch_us_per_step": tp.host_us_per_step,
+            "region_breakdown": getattr(tp, "breakdown", None),
             "single_stream": single,
             "forward_calls_per_s": world * args.steps / elapsed,
             "value_and_grad": grad_info,
