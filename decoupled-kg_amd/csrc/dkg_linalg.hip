@@ -22,6 +22,12 @@ constexpr int LB = 32;  // block width
 #ifndef DKG_CHOL_LDS_BCAST
 #define DKG_CHOL_LDS_BCAST 1
 #endif
+// The pivot's sqrt and the column's division correctly rounded, as LAPACK's potrf does.  v_rsq_f64 + one Newton
+// step saved ~0.02 ms of the 0.45 ms preparation but rounds differently; on the SMOKE surrogates (noise 1e-8,
+// conditioning ~1e10) that difference moved L-BFGS-B runs from the oracle's by 3e-5 (profiles/r04/exactpiv/).
+#ifndef DKG_CHOL_EXACT_PIVOT
+#define DKG_CHOL_EXACT_PIVOT 1
+#endif
 
 // Lower tile (ti, tj), tj <= ti, of the row-major enumeration t = ti (ti + 1) / 2 + tj.
 __device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
@@ -65,12 +71,18 @@ __device__ __forceinline__ void factor_diag(double* __restrict__ A, double* __re
         } else {
           // 1/sqrt(piv) by v_rsq_f64 and one Newton step, then L[j][j] = piv / sqrt(piv) and L[c][j] = a / sqrt(piv)
           // as products (the correctly rounded sqrt and division sequences made the step's dependent chain)
+#if DKG_CHOL_EXACT_PIVOT
+          // LAPACK's operations: the correctly rounded sqrt, and the column divided by it
+          const double dj = sqrt(piv);
+          a[j] = (lane == j) ? dj : a[j] / dj;
+#else
           double rq = __builtin_amdgcn_rsq(piv);
           rq = rq * fma(-0.5 * piv, rq * rq, 1.5);
           const double dj = piv * rq;
           // (entries above the diagonal take part unmasked: they are never read into the lower triangle, and the
           // rows are masked when the factor leaves the registers)
           a[j] = (lane == j) ? dj : a[j] * rq;
+#endif
 #if DKG_CHOL_LDS_BCAST
           // column j through LDS: one store, then every lane reads L[c][j] (c > j) back as broadcasts
           // (16-byte reads of two entries) instead of 31 v_readlane pairs.  Two buffers by column parity: a
