@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--graph-head", type=int, default=1,
                     help="--graph 2: each stream's period graph split into its first GRAPH_HEAD forwards and the rest, "
                          "the heads of all streams launched first (0 = one graph per stream)")
+    ap.add_argument("--stream-skew", type=int, default=0,
+                    help="--graph 2: move this many of the last-launched stream's forwards of a period to the first "
+                         "stream (it has work ~3 launches earlier); the results are the same rows either way")
     ap.add_argument("--launch-threads", type=int, default=1,
                     help="--graph 2: host threads enqueuing the streams' graphs side by side (dkg_launcher; "
                          "-1 = one per stream, 1 = the caller alone, in stream order)")
@@ -214,6 +217,7 @@ class Throughput:
         self.f32 = precision == "fp32"
         self.head = 0
         self.launch_threads = -1
+        self.skew = 0
 
     def run(self, ns, steps, warmup, graph, world):
         E, xchg, main_s, dev = self.E, self.xchg, self.main, self.dev
@@ -251,8 +255,14 @@ class Throughput:
             # after the launches of the whole graphs before it (a launch costs ~1 us of host per kernel)
             for slot in range(2):
                 gs = []
+                # stream i's rows r = i mod ns, less `skew` rows of the last stream moved to the first
+                own = [list(range(i, E, ns)) for i in range(ns)]
+                k = max(0, min(self.skew, len(own[-1]) - 1)) if ns > 1 else 0
+                if k:
+                    own[0] += own[-1][len(own[-1]) - k:]
+                    own[-1] = own[-1][:len(own[-1]) - k]
                 for i in range(ns):
-                    rows = list(range(i, E, ns))
+                    rows = own[i]
                     parts = [rows[:self.head], rows[self.head:]] if 0 < self.head < len(rows) else [rows]
                     pieces = []
                     for part in parts:
@@ -390,7 +400,7 @@ class Throughput:
                 "what": "an untimed replay of the timed region's launches (steps == E: one period), per stream "
                         "the GPU time at which each piece (its first `head` forwards, then the rest) had finished, "
                         "and the host time after each hipGraphLaunch, both from just before the first launch",
-                "forwards_per_stream": [len(range(i, E, ns)) for i in range(ns)],
+                "forwards_per_stream": [len(p) for p in own],
                 "host_launch_done_us": launch_us, "stream_piece_done_us": done,
                 "last_stream_done_us": max(d[-1] for d in done), "wall_us": round(wall_us, 1)}
         # this rank's device time of the forwards, and what the last exchange adds after them (exposed)
@@ -502,6 +512,7 @@ def main():
                         args.precision)
         tp.head = args.graph_head
         tp.launch_threads = args.launch_threads
+        tp.skew = args.stream_skew
         return w, model, D, X0, W, acq, tp
 
     w, model, D, X0, W, acq, tp = setup(args.workload)
