@@ -76,6 +76,22 @@ def _as_model_state(model) -> ModelListGPState:
 _BY_VALUE_NUMEL = 64  # tensors this small are fingerprinted by value as well
 
 
+_VIEWS: dict = {}  # id -> (tensor, data_ptr, numpy view of its memory): the by-value read without new tensors
+
+
+def _small_values(t):
+    """(data pointer, the bytes of the values) of a small CPU tensor, read through a cached numpy view of its
+    memory (~1 us against ~6 us for detach().tolist() per call: this runs on every forward)."""
+    p = t.data_ptr()
+    e = _VIEWS.get(id(t))
+    if e is None or e[0] is not t or e[1] != p:
+        if len(_VIEWS) > 256:
+            _VIEWS.clear()
+        e = (t, p, t.detach().numpy())
+        _VIEWS[id(t)] = e
+    return (p, e[2].tobytes())
+
+
 def _fingerprint(obj):
     """What the fitted state of ``model`` is made of, cheaply: every tensor by (identity, in-place
     version counter), every other field by value.  The reference reads the model live at every
@@ -86,7 +102,7 @@ def _fingerprint(obj):
             # hyperparameters (lengthscales, outputscale, noise, constant mean, Standardize buffers): by value,
             # since gpytorch's initialize() and constraint setters write them through .data, which does not
             # bump the version counter
-            return (id(obj), obj._version, tuple(obj.detach().reshape(-1).tolist()))
+            return (id(obj), obj._version) + _small_values(obj)
         return (id(obj), obj._version)
     if isinstance(obj, ModelListGPState):  # flat, no recursion: this runs on every forward
         return tuple((id(m.train_x), m.train_x._version, id(m.train_y), m.train_y._version,
