@@ -1,7 +1,7 @@
 #!/bin/bash
 # The SMOKE loop against the oracle run, default build and the exact-pivot Cholesky variant; state tests; prep time.
 set -uo pipefail
-out=${1:-gpurun_out/r04k}
+out=${1:-gpurun_out/exactpiv}
 mkdir -p "$out"
 ab=$GRAFT_REPO_ROOT/decoupled-kg_amd/dkg_amd/_native/ab
 for v in cur exactpiv; do

@@ -2,7 +2,7 @@
 # Envelope list refinement (DKG_ENV_REFINE, DKG_REFINE_OVERFLOW): forward + gradient parity suites, headline /
 # headline_nd pair and kernel stamps of the default build and each variant, then the variant A/B.
 set -uo pipefail
-out=${1:-gpurun_out/r04i}
+out=${1:-gpurun_out/refine_ab}
 mkdir -p "$out"
 ab=$GRAFT_REPO_ROOT/decoupled-kg_amd/dkg_amd/_native/ab
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_gpu_fused.py tests/test_gpu_epigraph.py \

@@ -2,7 +2,7 @@
 # The driver-shaped region (--steps 20 --warmup 5): its breakdown (bench.py region_breakdown) under the launch
 # variants (graph head 0/1/2, 3 or 4 streams), two runs each, interleaved.
 set -uo pipefail
-out=${1:-gpurun_out/r04j}
+out=${1:-gpurun_out/region}
 mkdir -p "$out"
 opts="--steps 20 --warmup 5 --cpu-seconds 0 --grad-steps 0 --b1-calls 0 --nd-steps 0 --stress-steps 0 --prep-reps 0"
 for rep in 1 2; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Driver-shaped region under stream skews (--stream-skew 0/1/2, graph head 1; skew 2 with head 0), three runs each.
 set -uo pipefail
-out=${1:-gpurun_out/r04l}
+out=${1:-gpurun_out/skew}
 mkdir -p "$out"
 opts="--steps 20 --warmup 5 --cpu-seconds 0 --grad-steps 0 --b1-calls 0 --nd-steps 0 --stress-steps 0 --prep-reps 0"
 for rep in 1 2 3; do
