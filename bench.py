@@ -78,8 +78,12 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0: the process's CPU affinity (os.sched_getaffinity), capped by OMP_NUM_THREADS if set")
     ap.add_argument("--profile-reps", type=int, default=50)
-    ap.add_argument("--streams", type=int, default=4,
-                    help="forward batches in flight: step k runs on stream k %% streams with its own plan workspace")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="launches in flight: launch u of an exchange period runs on stream u %% streams with its own "
+                         "plan workspace")
+    ap.add_argument("--batches-per-launch", type=int, default=0,
+                    help="forward batches per launch (dkg_plan_forward_batches, bit-identical to one forward per "
+                         "batch); 0 = auto: the largest divisor of the exchange period <= min(32, period / streams)")
     ap.add_argument("--graph", type=int, default=2,
                     help="1 = replay each full exchange period (E forwards over the streams) as one captured HIP "
                          "graph; 2 = one single-stream graph per stream per period, replayed side by side")
@@ -203,15 +207,22 @@ def hip_check(rc: int, what: str) -> None:
 
 
 class Throughput:
-    """The timed throughput path: E forward batches per exchange, ``streams`` batches in flight, one
-    captured HIP graph per exchange buffer (DESIGN.md §6 "Forward batches in flight")."""
+    """The timed throughput path: E forward batches per exchange, ``G`` batches per launch
+    (``dkg_plan_forward_batches``: one launch per stage runs G forwards, each its own B candidates and its
+    own result row, bit for bit what G ``forward_into`` calls write), the launches of a period dealt over
+    ``streams`` HIP streams with one captured HIP graph per stream (DESIGN.md §6 "Forward batches in flight")."""
 
-    def __init__(self, acq, X, B, E, mode, S_local, dev, precision):
+    def __init__(self, acq, X, B, E, mode, S_local, dev, precision, G=1):
         from dkg_amd.dist import BatchExchange
 
         self.acq, self.B, self.E, self.dev = acq, B, E, dev
+        self.G = max(1, min(G, E))
+        if E % self.G:
+            raise ValueError(f"--batches-per-launch {G} does not divide the exchange period {E}")
         self.plan = acq._plan_for(B)
         self.Xd = X.to(dev).contiguous()
+        # every batch of a launch is the workload's B candidates (as every step of earlier rounds was)
+        self.XG = self.Xd.repeat(self.G, 1).contiguous()
         self.xchg = BatchExchange(B, E, mode, S_local=S_local, device=dev)
         self.main = torch.cuda.current_stream(dev)
         self.f32 = precision == "fp32"
@@ -219,70 +230,84 @@ class Throughput:
         self.launch_threads = -1
         self.skew = 0
 
-    def run(self, ns, steps, warmup, graph, world):
-        E, xchg, main_s, dev = self.E, self.xchg, self.main, self.dev
+    def chunks(self, k0, k1, G):
+        """(first step, batches, unit index in its period) of the launches covering steps k0 .. k1 - 1:
+        G batches each, cut at exchange-period ends."""
+        k = k0
+        while k < k1:
+            g = min(G, k1 - k, self.E - k % self.E)
+            yield k, g, (k % self.E) // G
+            k += g
+
+    def run(self, ns, steps, warmup, graph, world, G=None):
+        E, xchg, main_s, dev, B = self.E, self.xchg, self.main, self.dev, self.B
+        G = self.G if G is None else G
         streams = [main_s] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
-        plans = [self.plan] + [self.acq._state.plan(self.acq._W, self.acq._target, self.plan.max_B, f32=self.f32)
-                               for _ in range(ns - 1)]
+        plans = [self.acq._state.plan(self.acq._W, self.acq._target, G * B, f32=self.f32) for _ in range(ns)]
+        XG = self.XG
 
         def join():
             for s in streams[1:]:
                 main_s.wait_stream(s)
 
-        def step(k):
-            kg = xchg.row(k)
+        def launch(k, g, i, kg):
+            if g == 1:
+                plans[i].forward_into(self.Xd, kg)
+            else:
+                plans[i].forward_batches_into(XG[:g * B], kg, B)
+
+        def unit(k, g, u):
+            kg = xchg.block(k, g)
             if ns > 1 and k % E == 0:
                 for s in streams[1:]:
                     s.wait_stream(main_s)
-            with torch.cuda.stream(streams[k % ns]):
-                plans[k % ns].forward_into(self.Xd, kg)
-            if k % E == E - 1:
+            with torch.cuda.stream(streams[u % ns]):
+                launch(k, g, u % ns, kg)
+            if (k + g) % E == 0:
                 join()
-            xchg.done(k)
+            xchg.done(k + g - 1)
 
-        for k in range(warmup):
-            step(k)
+        for k, g, u in self.chunks(0, warmup, G):
+            unit(k, g, u)
         join()
         xchg.flush(warmup)
         torch.cuda.synchronize()
+        nunits = E // G
         graphs = []
         launcher = None
         if graph == 2 and steps >= E:
-            # per stream one single-stream graph of its rows r = i mod ns: replayed on its own stream, each
-            # enqueues its forwards as one batch (a graph forked over streams replays node by node)
-            # each stream's rows in two pieces, its first `head` forwards and the rest: the heads of all
+            # per stream one single-stream graph of its units u = i mod ns: replayed on its own stream, each
+            # enqueues its launches as one batch (a graph forked over streams replays node by node);
+            # each stream's units in two pieces, its first `head` units and the rest: the heads of all
             # streams are launched first, so every stream has work a few us into the period instead of
             # after the launches of the whole graphs before it (a launch costs ~1 us of host per kernel)
+            own = [list(range(i, nunits, ns)) for i in range(ns)]
+            kk = max(0, min(self.skew, len(own[-1]) - 1)) if ns > 1 else 0
+            if kk:  # `skew` units of the last stream moved to the first
+                own[0] += own[-1][len(own[-1]) - kk:]
+                own[-1] = own[-1][:len(own[-1]) - kk]
             for slot in range(2):
                 gs = []
-                # stream i's rows r = i mod ns, less `skew` rows of the last stream moved to the first
-                own = [list(range(i, E, ns)) for i in range(ns)]
-                k = max(0, min(self.skew, len(own[-1]) - 1)) if ns > 1 else 0
-                if k:
-                    own[0] += own[-1][len(own[-1]) - k:]
-                    own[-1] = own[-1][:len(own[-1]) - k]
                 for i in range(ns):
                     rows = own[i]
                     parts = [rows[:self.head], rows[self.head:]] if 0 < self.head < len(rows) else [rows]
                     pieces = []
                     for part in parts:
-                        g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, stream=streams[i] if i else torch.cuda.Stream(dev),
+                        g_ = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g_, stream=streams[i] if i else torch.cuda.Stream(dev),
                                               capture_error_mode="thread_local"):
-                            for r in part:
-                                plans[i].forward_into(self.Xd, xchg.bufs[slot][r])
-                        pieces.append(g)
+                            for u in part:
+                                launch(u * G, G, i, xchg.bufs[slot][u * G:(u + 1) * G].view(-1))
+                        pieces.append(g_)
                     gs.append(pieces)
                 graphs.append(gs)
             torch.cuda.synchronize()
             # replayed with hipGraphLaunch on the raw executable graphs (what CUDAGraph.replay calls, without
-            # its Python and stream-guard overhead: ~9 instead of ~18 us of host time per launch, which is
-            # what a short run's four launches cost before the last stream starts)
+            # its Python and stream-guard overhead: ~9 instead of ~18 us of host time per launch)
             hip = hip_runtime()
-            execs = [[[ctypes.c_void_p(g.raw_cuda_graph_exec()) for g in pieces] for pieces in gs] for gs in graphs]
+            execs = [[[ctypes.c_void_p(g_.raw_cuda_graph_exec()) for g_ in pieces] for pieces in gs] for gs in graphs]
             npieces = max(len(p) for gs in graphs for p in gs)
             sptrs = [ctypes.c_void_p(s.cuda_stream) for s in streams]
-            # the streams' graphs enqueued side by side, one host thread per stream (dkg_launcher)
             nthr = ns if self.launch_threads < 0 else max(1, min(ns, self.launch_threads))
             if nthr > 1:
                 from dkg_amd.launch import GraphLauncher
@@ -290,33 +315,33 @@ class Throughput:
                 launcher = GraphLauncher(nthr)
                 for slot in range(2):
                     launcher.prepare(slot, [s.cuda_stream for s in streams],
-                                     [[g.value for g in pieces] for pieces in execs[slot]])
+                                     [[g_.value for g_ in pieces] for pieces in execs[slot]])
             # the fork / join events, created once (torch's wait_stream creates an event per call)
             evs = [ctypes.c_void_p() for _ in range(ns)]
             for e in evs:
                 hip_check(hip.hipEventCreateWithFlags(ctypes.byref(e), 2), "hipEventCreateWithFlags")  # no timing
         elif graph and steps >= E:
-            # one graph per exchange buffer: the E forwards of a period, forked over the streams exactly
-            # as the eager path does; replayed on the main stream, so the collective after it orders as before
+            # one graph per exchange buffer: the period's launches forked over the streams exactly as the eager
+            # path does; replayed on the main stream, so the collective after it orders as before
             for slot in range(2):
-                g = torch.cuda.CUDAGraph()
+                g_ = torch.cuda.CUDAGraph()
                 # thread_local: the RCCL watchdog thread may query events while this thread captures
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with torch.cuda.graph(g_, capture_error_mode="thread_local"):
                     cs = torch.cuda.current_stream(dev)
                     lanes = [cs] + streams[1:]
                     for s in lanes[1:]:
                         s.wait_stream(cs)
-                    for r in range(E):
-                        with torch.cuda.stream(lanes[r % ns]):
-                            plans[r % ns].forward_into(self.Xd, xchg.bufs[slot][r])
+                    for u in range(nunits):
+                        with torch.cuda.stream(lanes[u % ns]):
+                            launch(u * G, G, u % ns, xchg.bufs[slot][u * G:(u + 1) * G].view(-1))
                     for s in lanes[1:]:
                         cs.wait_stream(s)
-                graphs.append(g)
+                graphs.append(g_)
             torch.cuda.synchronize()
         if graphs:
             # one untimed replay of every graph (the first launch of a graph uploads it)
-            for g in graphs:
-                for gi in (g if isinstance(g, list) else [g]):
+            for g_ in graphs:
+                for gi in (g_ if isinstance(g_, list) else [g_]):
                     for gp in (gi if isinstance(gi, list) else [gi]):
                         gp.replay()
             torch.cuda.synchronize()
@@ -332,12 +357,12 @@ class Throughput:
             for s in streams[1:]:
                 s.wait_stream(main_s)
         k0 = 0
-        host = 0.0  # host seconds inside the launch calls (replay / plan.forward_into)
+        host = 0.0  # host seconds inside the launch calls (replay / plan launches)
         if graphs:
             while k0 + E <= steps:
-                xchg.row(k0)
+                xchg.block(k0, 1)
                 th = time.perf_counter()
-                g = graphs[(k0 // E) % 2]
+                g_ = graphs[(k0 // E) % 2]
                 if graph == 2:
                     # fork: every stream after the main stream's work so far (the previous period's exchange);
                     # the first period starts on an idle device (synchronized above), so it needs none
@@ -356,13 +381,13 @@ class Throughput:
                         hip_check(hip.hipEventRecord(evs[i], sptrs[i]), "hipEventRecord")
                         hip_check(hip.hipStreamWaitEvent(sptrs[0], evs[i], 0), "hipStreamWaitEvent")
                 else:
-                    g.replay()
+                    g_.replay()
                 host += time.perf_counter() - th
                 xchg.done(k0 + E - 1)
                 k0 += E
-        for k in range(k0, steps):
+        for k, g, u in self.chunks(k0, steps, G):
             th = time.perf_counter()
-            step(k)
+            unit(k, g, u)
             host += time.perf_counter() - th
         join()
         evc = torch.cuda.Event(enable_timing=True)
@@ -378,8 +403,8 @@ class Throughput:
         self.breakdown = None
         if graphs and graph == 2 and launcher is None and steps == E:
             # where a one-period region's time goes: the same launches again, untimed, with an event on every
-            # stream after each of its pieces (the head forward(s), then the rest) and the host clock after each
-            # hipGraphLaunch; GPU times relative to an event on the main stream just before the first launch
+            # stream after each of its pieces and the host clock after each hipGraphLaunch; GPU times relative
+            # to an event on the main stream just before the first launch
             torch.cuda.synchronize()
             e_start = torch.cuda.Event(enable_timing=True)
             marks = [[torch.cuda.Event(enable_timing=True) for _ in range(npieces)] for _ in range(ns)]
@@ -398,9 +423,9 @@ class Throughput:
                      if p < len(execs[0][i])] for i in range(ns)]
             self.breakdown = {
                 "what": "an untimed replay of the timed region's launches (steps == E: one period), per stream "
-                        "the GPU time at which each piece (its first `head` forwards, then the rest) had finished, "
+                        "the GPU time at which each piece (its first `head` launches, then the rest) had finished, "
                         "and the host time after each hipGraphLaunch, both from just before the first launch",
-                "forwards_per_stream": [len(p) for p in own],
+                "forwards_per_stream": [len(p) * G for p in own], "batches_per_launch": G,
                 "host_launch_done_us": launch_us, "stream_piece_done_us": done,
                 "last_stream_done_us": max(d[-1] for d in done), "wall_us": round(wall_us, 1)}
         # this rank's device time of the forwards, and what the last exchange adds after them (exposed)
@@ -460,6 +485,16 @@ def stage_rooflines(plan, Xd, model_fb, reps, precision, pmc):
 STAGE_BOUND = {"cross_root_kernel": "mfma", "posterior_cov_kernel": "mfma", "envelope_kernel": "valu/latency"}
 
 
+def batches_per_launch(E: int, args) -> int:
+    """Forward batches per launch: --batches-per-launch, or the largest divisor of the exchange period E
+    that leaves every stream a launch of its own (E / streams) and is at most 32 (a 32-batch launch of the
+    headline already fills the device many times over: 8,192 envelope workgroups)."""
+    if args.batches_per_launch > 0:
+        return args.batches_per_launch
+    cap = max(1, min(32, E // max(1, args.streams)))
+    return max(g for g in range(1, cap + 1) if E % g == 0)
+
+
 def pmc_file(args) -> str:
     if args.pmc != "auto":
         return args.pmc
@@ -489,7 +524,7 @@ def main():
     from dkg_amd.synthetic import WORKLOADS, make_problem
     from dkg_amd.utils import sample_simplex
 
-    def setup(wname):
+    def setup(wname, G=None):
         w = WORKLOADS[wname]
         model, D, X0, W = make_problem(w)
         X = X0
@@ -509,7 +544,7 @@ def main():
                                         precision=args.precision)
         E = max(1, min(args.exchange_every, args.steps))
         tp = Throughput(acq, X, w.B, E, "gather" if args.shard == "candidates" else "reduce", w.S, dev,
-                        args.precision)
+                        args.precision, G=batches_per_launch(E, args) if G is None else G)
         tp.head = args.graph_head
         tp.launch_threads = args.launch_threads
         tp.skew = args.stream_skew
@@ -518,7 +553,7 @@ def main():
     w, model, D, X0, W, acq, tp = setup(args.workload)
     single = None
     if args.streams > 1 or args.graph:
-        e1 = tp.run(1, args.steps, args.warmup, False, world)
+        e1 = tp.run(1, args.steps, args.warmup, False, world, G=1)
         single = {"value": world * w.B * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3}
     elapsed = tp.run(max(1, args.streams), args.steps, args.warmup, args.graph, world)
     value = world * w.B * args.steps / elapsed
@@ -668,7 +703,7 @@ def main():
     # ---- stress leg: BASELINE configs[4]'s shape (m 3, n 1024, N 4096, S 32, B 256), fp64
     stress = None
     if args.stress_steps > 0 and args.workload == "headline" and args.precision == "fp64":
-        ws, ms, Ds, _, _, _, tps = setup("stress")
+        ws, ms, Ds, _, _, _, tps = setup("stress", G=1)
         es = tps.run(1, args.stress_steps, 2, False, world)
         fb = stage_model(ws, ws.m, [mm.num_train for mm in ms.models], Ds.shape[0], ws.B, ws.S, ws.d)
         # the stress workload's own PMC file (profiles/r04/pmc_stress.json) for its stages' traffic / busy figures
@@ -712,6 +747,10 @@ def main():
                                       f"{'all-gather' if args.shard == 'candidates' else 'all-reduce'} "
                                       f"per {E} forward batches",
                        "exchange_every": E, "streams": max(1, args.streams),
+                       "batches_per_launch": tp.G,
+                       "launch": f"{tp.G} forward batch(es) of {w.B} candidates per launch of each stage "
+                                 "(dkg_plan_forward_batches: each batch its own candidates and result row, the "
+                                 "same bits as one forward per batch)",
                        "hip_graph": {0: "off", 1: "one graph forked over the streams",
                                      2: "one single-stream graph per stream"}.get(args.graph, str(args.graph))
                        + (f" (first {args.graph_head} forward(s) of every stream launched first)"

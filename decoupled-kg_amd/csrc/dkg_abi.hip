@@ -91,7 +91,7 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
     L.q[i] = off;
     off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
     L.kx[i] = 0;
-    if (cross_kfill(max_np_of(outs, m))) {  // the launch covers every output of the plan
+    if (cross_kfill_launch(max_np_of(outs, m), B)) {  // the launch covers every output of the plan
       L.kx[i] = off;
       off = align256(off + Bp * pad16(outs[i].n) * sizeof(double));
     }
@@ -583,6 +583,21 @@ int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* 
   if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
   return run_forward(*static_cast<const Plan*>(host_plan), static_cast<const Plan*>(dev_plan), xnew, B, kg, kg_pairs,
                      (hipStream_t)stream, nullptr);
+}
+
+int dkg_plan_forward_batches(const void* host_plan, const void* dev_plan, const double* xnew, int B, int nbatch,
+                             double* kg, void* stream) {
+  if (!host_plan || !dev_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  const Plan& h = *static_cast<const Plan*>(host_plan);
+  if (B < 0 || nbatch < 0) return fail(DKG_ERR_ARG, "negative size B=%d nbatch=%d", B, nbatch);
+  if ((long long)B * nbatch == 0) return DKG_OK;
+  if ((long long)B * nbatch > h.max_B)
+    return fail(DKG_ERR_ARG, "%d batches x B=%d candidates > plan capacity %d", nbatch, B, h.max_B);
+  if (!xnew || !kg) return fail(DKG_ERR_ARG, "NULL data pointer");
+  // the three stage kernels over all nbatch * B candidates, the covariance blocks chosen for one batch of B
+  return hip_check(launch_forward(h, static_cast<const Plan*>(dev_plan), xnew, B * nbatch, kg, nullptr,
+                                  (hipStream_t)stream, nullptr, B),
+                   "forward_batches");
 }
 
 int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,

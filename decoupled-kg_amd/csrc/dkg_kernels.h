@@ -37,6 +37,13 @@ constexpr int DUP_NONE = 0x7fffffff;
 #define DKG_CROSS_KFILL 1
 #endif
 __host__ __device__ inline bool cross_kfill(int np) { return DKG_CROSS_KFILL && np >= 512; }
+// Launches over many candidates (a launch of several forward batches, dkg_plan_forward_batches) fill K(x, X)
+// once with the separate kernel at any n: the fill replicated over the column-pair groups of a row tile (~4.5x
+// at n = 256) is then work the whole device waits on, not latency one forward hides.  Same bits either way.
+constexpr int KFILL_MIN_B = 512;
+__host__ __device__ inline bool cross_kfill_launch(int np, int B) {
+  return DKG_CROSS_KFILL && (np >= 512 || B >= KFILL_MIN_B);
+}
 
 // Register slots per lane for a staged (non-streaming) line set of `lines`
 // lines: the envelope_kernel instantiation launch_env_bucket picks.
@@ -145,11 +152,13 @@ struct XArg {
 hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* dkg,
                                hipStream_t s, const XArg* xa = nullptr, double* hout = nullptr);
 size_t envelope_grad_lds_bytes(int m, int N, int waves, int S, int d, int max_np, bool stream);
-// One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.
+// One stage of the forward (0 cross_root, 1 posterior_cov, 2 envelope) on stream s.  geom_B (0: B) is the
+// batch size the covariance block shape is chosen for: a launch over K batches of geom_B candidates
+// (dkg_plan_forward_batches) takes the blocks of one geom_B forward, so its results are those of K forwards.
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
-                        hipStream_t s, int stage);
+                        hipStream_t s, int stage, int geom_B = 0);
 hipError_t launch_forward(const Plan& host, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
-                          hipStream_t s, hipEvent_t* ev);
+                          hipStream_t s, hipEvent_t* ev, int geom_B = 0);
 // The fused one-launch forward (dkg_fused.h) when the plan allows it (Plan::fused, no kg_pairs);
 // otherwise the three stage kernels.  Same bits.
 // Dynamic LDS bytes of the fused forward for a plan (dkg_fused.h fused_lds_bytes).

@@ -180,31 +180,38 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_kernel(CrossArgs a
   cross_root_impl<DM>(a.o, a.d, a.x, a.rows, a.q, a.mean, blockIdx.x, blockIdx.y, smem);
 }
 
-// Forward: grid (B tiles, pairs, outputs); workgroup (0,0,0) also clears the
-// KG accumulators (and arrival tickets) the envelope stage adds into, and the
-// candidates' coincidence marks (Plan::dup) the covariance stage sets.
+// The KG accumulators (and arrival tickets) the envelope stage adds into and the coincidence marks
+// (Plan::dup) the covariance stage sets, cleared for row tile ti's 16 candidates: each tile's first
+// workgroup clears its own rows, so a launch over many batches (dkg_plan_forward_batches) spreads the
+// clearing instead of one workgroup looping over every candidate.
+__device__ inline void clear_tile_accumulators(const Plan* __restrict__ P, double* __restrict__ kg, int B, int ti) {
+  const int b0 = ti * 16, b1 = min(B, b0 + 16), ng1 = pair_groups(P->S) + 1;
+  for (int i = b0 + (int)threadIdx.x; i < b1; i += blockDim.x) {
+    kg[i] = 0.0;
+    P->dup[i] = DUP_NONE;
+  }
+  for (int i = b0 * ng1 + (int)threadIdx.x; i < b1 * ng1; i += blockDim.x) P->tickets[i] = 0;
+}
+
+// Forward: grid (B tiles, pairs, outputs); the first workgroup of every row tile also clears that
+// tile's accumulators (clear_tile_accumulators).
 template <int DM, class T = double>
 __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_root_plan_kernel(const Plan* __restrict__ P,
                                                                           const double* __restrict__ xnew, int B,
-                                                                          double* __restrict__ kg, int dst) {
+                                                                          double* __restrict__ kg, int dst,
+                                                                          int use_kx) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   unsigned long long* st = kst_slot(dst, P, 0);
   KST_BEGIN(st);
   const int oi = blockIdx.z;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && oi == 0) {
-    for (int i = threadIdx.x; i < B; i += blockDim.x) {
-      kg[i] = 0.0;
-      P->dup[i] = DUP_NONE;
-    }
-    for (int i = threadIdx.x; i < B * (pair_groups(P->S) + 1); i += blockDim.x) P->tickets[i] = 0;
-  }
+  if (blockIdx.y == 0 && oi == 0) clear_tile_accumulators(P, kg, B, blockIdx.x);
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_cov) & 2)) return;  // ablation: empty cross stage
   if constexpr (sizeof(T) == 8) {
     cross_root_impl<DM>(P->o[oi], P->d, xnew, B, P->q[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem, st, 0,
-                        P->kx[oi]);
+                        use_kx ? P->kx[oi] : nullptr);
   } else {
     cross_root_impl<DM, false, float>(P->o[oi], P->d, xnew, B, P->q32[oi], P->mux[oi], blockIdx.x, blockIdx.y, smem,
-                                      st, 0, P->kx[oi], nullptr, P->root32[oi]);
+                                      st, 0, use_kx ? P->kx[oi] : nullptr, nullptr, P->root32[oi]);
   }
 }
 
@@ -242,13 +249,7 @@ __global__ __launch_bounds__(CR_WAVES * WAVE) void cross_fwd_grad_kernel(const P
       for (int i = threadIdx.x; i < xa.n; i += blockDim.x) xstage[i] = xa.v[i];
   }
   if (z < m) {
-    if (blockIdx.x == 0 && blockIdx.y == 0 && z == 0) {
-      for (int i = threadIdx.x; i < B; i += blockDim.x) {
-        kg[i] = 0.0;
-        P->dup[i] = DUP_NONE;
-      }
-      for (int i = threadIdx.x; i < B * (pair_groups(P->S) + 1); i += blockDim.x) P->tickets[i] = 0;
-    }
+    if (blockIdx.y == 0 && z == 0) clear_tile_accumulators(P, kg, B, blockIdx.x);
     cross_root_impl<DM>(P->o[z], d, xnew, B, P->q[z], P->mux[z], blockIdx.x, blockIdx.y, smem, st, 0, nullptr,
                         P->qxrm[z]);
     return;
@@ -470,9 +471,10 @@ static bool cov_wide(int N, int B, int m) {
 
 template <int DM, class T>
 static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
-                                      hipStream_t s, int stage) {
+                                      hipStream_t s, int stage, int geom_B) {
   if (stage == 0) {
-    if (h.kx[0] != nullptr) {
+    const int use_kx = (h.kx[0] != nullptr && cross_kfill_launch(h.max_np, B)) ? 1 : 0;
+    if (use_kx) {
       dim3 kgrid(pad16(B) / 16, (h.max_np / 4 + KF_KB - 1) / KF_KB, h.m);
       hipLaunchKernelGGL((cross_kfill_kernel<DM>), kgrid, dim3(KF_WAVES * WAVE), 0, s, dev, xnew, B);
     }
@@ -480,11 +482,11 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
     raise_lds_limit((const void*)cross_root_plan_kernel<DM, T>, lds);
     hipLaunchKernelGGL((cross_root_plan_kernel<DM, T>), grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
-                       h.debug_stamp);
+                       h.debug_stamp, use_kx);
     return hipGetLastError();
   }
   if constexpr (sizeof(T) == 8 && DM <= 4) {
-    if (cov_wide(h.N, B, h.m)) {
+    if (cov_wide(h.N, geom_B, h.m)) {
       dim3 grid(xcd_group_size(((h.N + 63) / 64) * ((B + 63) / 64), h.m));
       hipLaunchKernelGGL((posterior_cov_wide_kernel<DM>), grid, dim3(PW_WAVES * WAVE), 0, s, dev, xnew, B,
                          h.debug_stamp);
@@ -498,9 +500,9 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
 
 template <int DM>
 static hipError_t launch_cross_cov_t(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
-                                     hipStream_t s, int stage) {
-  return h.f32 ? launch_cross_cov_tt<DM, float>(h, dev, xnew, B, kg, s, stage)
-               : launch_cross_cov_tt<DM, double>(h, dev, xnew, B, kg, s, stage);
+                                     hipStream_t s, int stage, int geom_B) {
+  return h.f32 ? launch_cross_cov_tt<DM, float>(h, dev, xnew, B, kg, s, stage, geom_B)
+               : launch_cross_cov_tt<DM, double>(h, dev, xnew, B, kg, s, stage, geom_B);
 }
 
 // Narrow small-batch geometry: off (DKG_ENV_NARROW=0).  At B = 1 its 16 one-wave workgroups staged the lines
@@ -539,13 +541,14 @@ static hipError_t launch_env(const Plan& h, const EnvLaunch& a) {
 }
 
 hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
-                        hipStream_t s, int stage) {
+                        hipStream_t s, int stage, int geom_B) {
   if (stage == 0 || stage == 1) {
+    const int gb = geom_B > 0 ? geom_B : B;
     switch (dim_bucket(h.d)) {
-      case 2: return launch_cross_cov_t<2>(h, dev, xnew, B, kg, s, stage);
-      case 4: return launch_cross_cov_t<4>(h, dev, xnew, B, kg, s, stage);
-      case 8: return launch_cross_cov_t<8>(h, dev, xnew, B, kg, s, stage);
-      default: return launch_cross_cov_t<16>(h, dev, xnew, B, kg, s, stage);
+      case 2: return launch_cross_cov_t<2>(h, dev, xnew, B, kg, s, stage, gb);
+      case 4: return launch_cross_cov_t<4>(h, dev, xnew, B, kg, s, stage, gb);
+      case 8: return launch_cross_cov_t<8>(h, dev, xnew, B, kg, s, stage, gb);
+      default: return launch_cross_cov_t<16>(h, dev, xnew, B, kg, s, stage, gb);
     }
   }
   EnvLaunch a{&h, dev, B, kg, pairs, dim3(xcd_group_size(B, h.split)), dim3(h.sw * WAVE),
@@ -586,10 +589,10 @@ hipError_t launch_forward_grad(const Plan& h, const Plan* dev, const double* xne
 }
 
 hipError_t launch_forward(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg, double* pairs,
-                          hipStream_t s, hipEvent_t* ev) {
+                          hipStream_t s, hipEvent_t* ev, int geom_B) {
   for (int stage = 0; stage < 3; ++stage) {
     if (ev) (void)hipEventRecord(ev[stage], s);
-    const hipError_t e = launch_stage(h, dev, xnew, B, kg, pairs, s, stage);
+    const hipError_t e = launch_stage(h, dev, xnew, B, kg, pairs, s, stage, geom_B);
     if (e != hipSuccess) return e;
   }
   if (ev) (void)hipEventRecord(ev[3], s);

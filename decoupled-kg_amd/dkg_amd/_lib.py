@@ -17,7 +17,7 @@ from .errors import BotorchTensorDimensionError, DkgNativeError, NotPSDError, Un
 LIB_PATH = os.environ.get("DKG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native",
                                                      "libdkg.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 DKG_XARG_MAX = 64  # include/dkg.h: largest B * d of dkg_plan_forward_grad_hostx
 DKG_PLAN_GRAD = 1
 DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
@@ -80,6 +80,7 @@ SIGNATURES = {
     "dkg_plan_forward_grad_hostx": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                             c_void_p, c_void_p]),
     "dkg_plan_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "dkg_plan_forward_batches": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "dkg_plan_forward_timed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                        POINTER(c_float)]),
     "dkg_plan_time_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,

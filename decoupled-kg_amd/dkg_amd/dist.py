@@ -296,6 +296,16 @@ class BatchExchange:
             self._finish(slot)
         return self.bufs[slot][r]
 
+    def block(self, k: int, g: int) -> Tensor:
+        """The [g * B] buffer steps k .. k + g - 1 write (one launch of g forward batches,
+        ``ForwardPlan.forward_batches_into``): rows of one buffer, so they may not cross an exchange."""
+        slot, r = self._slot(k)
+        if g < 1 or r + g > self.E:
+            raise ValueError(f"steps {k}..{k + g - 1} cross an exchange of {self.E} steps")
+        if r == 0:
+            self._finish(slot)
+        return self.bufs[slot][r:r + g].view(-1)
+
     def _exchange(self, slot: int, rows: int) -> None:
         self.rows[slot] = rows
         if self.world == 1:

@@ -207,6 +207,7 @@ class ForwardPlan:
                    "dkg_plan_init")
         self.fused = bool(lib.dkg_plan_fused(self.host))  # forward_into is one fused launch
         self._fwd = lib.dkg_plan_forward
+        self._fwd_batches = lib.dkg_plan_forward_batches
         self._fwd_timed = lib.dkg_plan_forward_timed
         self._fwd_grad_hostx = lib.dkg_plan_forward_grad_hostx
         self._dev_ptr = _lib.ptr(self.dev)
@@ -234,6 +235,18 @@ class ForwardPlan:
                        torch.cuda.current_stream(self.device).cuda_stream)
         if st:
             _lib.check(st, "dkg_plan_forward")
+
+    def forward_batches_into(self, X: torch.Tensor, kg: torch.Tensor, B: int) -> None:
+        """K = X.shape[0] // B forward batches of B candidates in one launch per stage
+        (``dkg_plan_forward_batches``): X (device, K*B x d, contiguous fp64, batch k = rows kB .. kB+B-1)
+        -> kg (device, K*B).  Bit-for-bit the results of K ``forward_into`` calls, one per batch."""
+        n = X.shape[0]
+        if B < 1 or n % B:
+            raise ValueError(f"{n} candidates are not whole batches of {B}")
+        st = self._fwd_batches(self.host, self._dev_ptr, X.data_ptr(), B, n // B, kg.data_ptr(),
+                               torch.cuda.current_stream(self.device).cuda_stream)
+        if st:
+            _lib.check(st, "dkg_plan_forward_batches")
 
     def forward_stats(self, X: torch.Tensor):
         """One forward with diagnostics: KG [B], KG per (candidate, scalarisation) [B, S] and the number

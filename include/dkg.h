@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 7  /* 7: plan flag DKG_PLAN_NO_CHAIN; the plan holds the large-n K(x, X) fill pointers */
+#define DKG_ABI_VERSION 8  /* 8: dkg_plan_forward_batches; 7: plan flag DKG_PLAN_NO_CHAIN */
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -199,6 +199,15 @@ int dkg_plan_init(const dkg_output* outs, int m, int d, const double* disc, int 
  * with DKG_PLAN_FUSED (a call given kg_pairs runs the three stages). */
 int dkg_plan_forward(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                      double* kg_pairs, void* stream);
+/* nbatch forward batches of B candidates in one launch per stage: xnew is device [nbatch][B][d], kg
+ * device [nbatch][B], nbatch * B <= max_B.  kg[k][b] is bit-for-bit what dkg_plan_forward of batch k
+ * alone writes (every candidate's result depends on its own x only, and the covariance blocks are the
+ * ones a B-candidate forward takes), so this is nbatch dkg_plan_forward calls with 3 launches instead
+ * of 3 * nbatch: the throughput form of the reference's per-batch forward (discretekg.py:131-159) when
+ * a caller has several batches ready (bench.py's steps).  Always the three stage kernels (a fused plan
+ * included). */
+int dkg_plan_forward_batches(const void* host_plan, const void* dev_plan, const double* xnew, int B, int nbatch,
+                             double* kg, void* stream);
 /* As dkg_plan_forward with per-kernel HIP-event timings (synchronises): stage_ms[3]. */
 int dkg_plan_forward_timed(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                            double* kg_pairs, void* stream, float* stage_ms);

@@ -15,8 +15,9 @@ from oracle.discretekg import (calculate_discrete_kg, calculate_discrete_kg_cond
 
 NAMES = ["lengthscales0", "observationnoise0"]
 # the oracle's own lines against the committed ones (CPU): the host-BLAS summation-order gap, not the
-# device-vs-oracle LINE_RTOL
-GOLDEN_LINE_RTOL = 1e-10
+# device-vs-oracle LINE_RTOL (0 in the build container, 6e-13 and 3.8e-10 of the largest line on two GPU
+# boxes' hosts, whose BLAS sums K(D, D)'s ill-conditioned solves in other orders)
+GOLDEN_LINE_RTOL = 1e-9
 PATHS = [("full", None), ("t0", 0), ("t1", 1)]
 
 
@@ -32,8 +33,7 @@ def test_oracle_reproduces_golden(name):
     assert_within(got_full, t["kg_full"][idx], stated_tol(t["kg_full"][idx], amax_full))
     assert_within(got_t1, t["kg_t1"][idx], stated_tol(t["kg_t1"][idx], amax_t1))
     # the lines themselves: a BLAS summing in another order, through the conditioning of K(D, D),
-    # moves them by ~1e-13 of the largest line (6e-12 at max|a| = 10 on the MI355X box's host, 0 in the
-    # build container): GOLDEN_LINE_RTOL, a little above that gap, so drift in the restatement shows
+    # moves them (GOLDEN_LINE_RTOL above); drift in the restatement itself shows far above that
     a, b = lines_batched(om, X[:4], D, W, None)
     for got, ref in ((a, t["lines_a"]), (b, t["lines_b"])):
         scale = ref.abs().amax((-1, -2), keepdim=True)

@@ -1,0 +1,83 @@
+"""K forward batches in one launch per stage (include/dkg.h dkg_plan_forward_batches).
+
+Each batch keeps its own candidates and its own result row: the batched launch must write, bit for bit,
+what one dkg_plan_forward per batch writes (the reference's forward is per batch, discretekg.py:131-159).
+Covers batch sizes that are not multiples of the 16-candidate tiles, the decoupled path, candidates on
+discretisation points (the per-tile clearing of the coincidence marks), a launch large enough that the
+whole launch would take the other covariance block shape (the block shape is chosen per batch), and the
+stress shape (64 x 64 covariance blocks).
+"""
+
+import pytest
+import torch
+
+from dkg_amd import DiscreteKnowledgeGradient
+from dkg_amd.errors import BotorchTensorDimensionError
+from dkg_amd.synthetic import WORKLOADS, make_problem
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def _batched_vs_single(wname, B, K, target, on_grid=0, seed=3):
+    model, D, _, W = make_problem(WORKLOADS[wname])
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    d = D.shape[1]
+    X = torch.quasirandom.SobolEngine(d, scramble=True, seed=seed).draw(K * B, dtype=torch.double)
+    if on_grid:  # some candidates exactly on discretisation points, in the middle batch
+        k = K // 2
+        X[k * B:k * B + on_grid] = D[torch.arange(on_grid) * 7 % D.shape[0]]
+    X = X.to(DEV)
+    big = acq._state.plan(acq._W, acq._target, K * B)
+    one = acq._state.plan(acq._W, acq._target, B)
+    kg = torch.full((K * B,), float("nan"), dtype=torch.double, device=DEV)
+    big.forward_batches_into(X, kg, B)
+    ref = torch.full_like(kg, float("nan"))
+    for j in range(K):
+        one.forward_into(X[j * B:(j + 1) * B], ref[j * B:(j + 1) * B])
+    # twice: the second launch on the same plan must not see the first one's accumulators or marks
+    kg2 = torch.full_like(kg, float("nan"))
+    big.forward_batches_into(X, kg2, B)
+    torch.cuda.synchronize()
+    return kg.cpu(), kg2.cpu(), ref.cpu()
+
+
+@pytest.mark.parametrize("wname,B,K,target,on_grid", [
+    ("headline", 128, 20, None, 0),    # 2,560 candidates: as one forward it would take the 64 x 64 blocks
+    ("headline", 128, 4, 0, 5),
+    ("small", 37, 5, None, 3),         # batches straddle the 16-candidate tiles
+    ("small", 1, 9, 1, 1),
+    ("parity6d", 23, 3, None, 0),
+    ("headline_nd", 128, 3, 1, 0),
+])
+def test_batched_launch_writes_the_per_batch_bits(wname, B, K, target, on_grid):
+    kg, kg2, ref = _batched_vs_single(wname, B, K, target, on_grid)
+    assert not torch.isnan(ref).any()
+    assert torch.equal(kg, ref)
+    assert torch.equal(kg2, ref)
+    if wname != "headline" or on_grid:
+        assert (ref > 0).any()
+
+
+def test_batched_launch_stress_shape():
+    kg, kg2, ref = _batched_vs_single("stress", 256, 2, None, 0)
+    assert torch.equal(kg, ref) and torch.equal(kg2, ref)
+
+
+def test_batched_launch_arguments():
+    model, D, X0, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    plan = acq._state.plan(acq._W, acq._target, 64)
+    X = X0.to(DEV).repeat(3, 1).contiguous()
+    kg = torch.empty(96, dtype=torch.double, device=DEV)
+    with pytest.raises(ValueError):
+        plan.forward_batches_into(X[:95], kg, 32)          # not whole batches
+    with pytest.raises(BotorchTensorDimensionError):  # DKG_ERR_ARG
+        plan.forward_batches_into(X, kg, 32)               # 96 > plan capacity 64
+    plan.forward_batches_into(X[:0], kg, 32)               # no batches: nothing to do
