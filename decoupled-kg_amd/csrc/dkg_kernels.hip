@@ -469,6 +469,15 @@ static bool cov_wide(int N, int B, int m) {
   return N >= 64 && B >= 64 && (size_t)((N + 63) / 64) * ((B + 63) / 64) * m >= 512;
 }
 
+// The LDS-staged 64 x 128 blocks (posterior_cov_big_kernel: posterior_cov_kernel's bits) once a launch has at
+// least one block per CU; decided on the launch's whole candidate count (a launch of several forward batches
+// takes them whatever one batch would).  DKG_COV_BIG=0 / 1 (A/B measurements) forces the choice.
+static bool cov_big(int N, int B, int m) {
+  static const char* env = std::getenv("DKG_COV_BIG");
+  if (env) return std::atoi(env) != 0 && N >= 1;
+  return N >= 128 && (size_t)((N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)) * m >= 256;
+}
+
 template <int DM, class T>
 static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
                                       hipStream_t s, int stage, int geom_B) {
@@ -484,6 +493,15 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
     hipLaunchKernelGGL((cross_root_plan_kernel<DM, T>), grid, dim3(CR_WAVES * WAVE), lds, s, dev, xnew, B, kg,
                        h.debug_stamp, use_kx);
     return hipGetLastError();
+  }
+  if constexpr (sizeof(T) == 8 && DM <= 8) {  // (d > 8: the big blocks' kernel terms spill)
+    if (cov_big(h.N, B, h.m)) {
+      dim3 grid(xcd_group_size(((h.N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)), h.m));
+      raise_lds_limit((const void*)posterior_cov_big_kernel<DM>, PB_LDS);
+      hipLaunchKernelGGL((posterior_cov_big_kernel<DM>), grid, dim3(PB_WAVES * WAVE), PB_LDS, s, dev, xnew, B,
+                         h.debug_stamp);
+      return hipGetLastError();
+    }
   }
   if constexpr (sizeof(T) == 8 && DM <= 4) {
     if (cov_wide(h.N, geom_B, h.m)) {

@@ -46,6 +46,9 @@ struct Launcher {
   std::atomic<int64_t> spin_until_ns{0};
   std::mutex mu;
   std::condition_variable cv;
+  // one dkg_launcher_graphs call at a time: the call's launch set lives in the fields below and the
+  // workers' pending count is per call, so concurrent callers would overwrite each other's sets
+  std::mutex call_mu;
   // the current call: stream s launches graphs[offs[s] .. offs[s+1]) on streams[s]; thread t takes the
   // streams s with s % nthreads == t
   int n_streams = 0;
@@ -139,6 +142,7 @@ int dkg_launcher_graphs(void* h, int n_streams, void* const* streams, const int*
     return dkg::fail(DKG_ERR_ARG, "bad launcher arguments");
   for (int s = 0; s < n_streams; ++s)
     if (offs[s + 1] < offs[s]) return dkg::fail(DKG_ERR_ARG, "graph offsets not increasing at stream %d", s);
+  std::lock_guard<std::mutex> call(L->call_mu);
   L->n_streams = n_streams;
   L->streams = streams;
   L->offs = offs;

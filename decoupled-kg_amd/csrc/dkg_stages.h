@@ -684,6 +684,173 @@ __global__ __launch_bounds__(PW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   KST_END(st);
 }
 
+// ---------------------------------------------------------------------------
+// posterior_cov_big_kernel (fp64): the covariance rows of launches over many candidates (forward batches in
+// one launch, dkg_plan_forward_batches; the stress shape) with posterior_cov_kernel's arithmetic element for
+// element, so the two give the same bits and the choice between them is a speed matter only.
+// posterior_cov_kernel sums each element as two K halves (words [0, KPs) and [KPs, KP)), each over four
+// chains of k-blocks (k-block index from the half's start mod 4, in increasing order), combined
+// (c0 + c1) + (c2 + c3), then half 0 + half 1; its variance sums likewise per half (lane-wise FMAs in k order,
+// then the xor-16 / xor-32 exchange), half 0 + half 1.  At 32 x 32 blocks every 16-byte operand load feeds two
+// MFMAs and the L1 path, not the MFMA, sets the rate once a launch fills the device (37 % of the fp64 roof
+// at 20 headline batches).  Here a workgroup of 8 waves (2 per SIMD) owns a 64 x 128 block (4 candidate
+// tiles x 8 line tiles of one output); the operand tiles are staged once per workgroup through LDS by
+// LDS-DMA in chunks of PB_WC words (double-buffered, the next chunk in flight during the current one's
+// MFMAs), and each wave computes a 2 x 2 group of tiles over both halves in turn (16 accumulator chains),
+// reading its fragments from LDS with one 16-byte read per two MFMAs per operand tile.
+constexpr int PB_WAVES = 8;
+constexpr int PB_RT = 4;  // candidate tiles per block
+constexpr int PB_CT = 8;  // line tiles per block
+constexpr int PB_WC = 4;  // words (two k-blocks each) per staged chunk; even, so chains restart in step
+constexpr int PB_STAGE = (PB_RT + PB_CT) * PB_WC * 64;  // 16-byte words per stage buffer
+constexpr size_t PB_LDS = 2 * (size_t)PB_STAGE * 16;     // double-buffered: 96 KiB
+
+template <int DM>
+__global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_big_kernel(
+    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double2* stg = reinterpret_cast<double2*>(smem);
+  const int N = P->N;
+  const int nbx = (N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
+  int blk, oi;
+  if (!xcd_group(blockIdx.x, nbx * nby, P->m, blk, oi)) return;
+  unsigned long long* st = kst_slot(dst, P, 1);
+  KST_BEGIN(st);
+  const int bx = blk % nbx, by = blk / nbx;
+  const dkg_output& o = P->o[oi];
+  const int d = P->d;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rp = wave & 1, cp = wave >> 1;  // the wave's tiles: rows 2 rp, 2 rp + 1; columns 2 cp, 2 cp + 1
+  const int RT = pad16(B) / 16, CT = pad16(N) / 16;
+  const int KB = pad16(o.n) / 4, KP = KB / 2, KPs = (KP + 1) / 2;  // posterior_cov_body's halves (PC_KS = 2)
+  const int ti0 = PB_RT * by, tk0 = PB_CT * bx;
+  const double* qx = P->q[oi];
+  const double* qd = o.disc_frag;
+  // chunks: half 0's words [0, KPs), then half 1's [KPs, KP), PB_WC words each, starting at each half's start
+  const int nc0 = (KPs + PB_WC - 1) / PB_WC, nc = nc0 + (KP - KPs + PB_WC - 1) / PB_WC;
+  auto chunk_start = [&](int c) { return c < nc0 ? c * PB_WC : KPs + (c - nc0) * PB_WC; };
+  auto chunk_words = [&](int c) { return c < nc0 ? min(PB_WC, KPs - c * PB_WC) : min(PB_WC, KP - chunk_start(c)); };
+  // chunk c's words of the block's tiles into buffer c & 1 (tiles past the matrix read its last tile: discarded)
+  auto stage = [&](int c) {
+    const int j0 = chunk_start(c), nw = chunk_words(c);
+    double2* buf = stg + (size_t)(c & 1) * PB_STAGE;
+    for (int piece = wave; piece < (PB_RT + PB_CT) * PB_WC; piece += PB_WAVES) {
+      const int t = piece / PB_WC, w = piece % PB_WC;
+      if (w >= nw) continue;  // wave-uniform
+      const double* src = t < PB_RT ? qx : qd;
+      const int tile = t < PB_RT ? min(ti0 + t, RT - 1) : min(tk0 + t - PB_RT, CT - 1);
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const void*>(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 2),
+          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(buf + piece * 64)),
+          16, 0, 0);
+    }
+  };
+  const bool want_var = bx == 0 && cp == 0;  // the wave's column tiles include tile 0: its row tiles' variances
+  d4 acc[2][2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[h][g][c] = d4{0.0, 0.0, 0.0, 0.0};
+  d4 sum0[2][2];
+  double qsq[2] = {0.0, 0.0}, qh0[2] = {0.0, 0.0};
+  stage(0);
+  KST(st, 2);
+  for (int c = 0; c < nc; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // chunk c landed; every wave is done with the other buffer
+    if (c + 1 < nc) stage(c + 1);
+    if (c == nc0) {  // half 0 done: its sums, and the chains restart for half 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          sum0[h][g] = (acc[h][g][0] + acc[h][g][1]) + (acc[h][g][2] + acc[h][g][3]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[h][g][q] = d4{0.0, 0.0, 0.0, 0.0};
+        }
+      if (want_var) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          double q = qsq[h];
+          q += __shfl_xor(q, 16);
+          q += __shfl_xor(q, 32);
+          qh0[h] = q;
+          qsq[h] = 0.0;
+        }
+      }
+    }
+    const double2* buf = stg + (size_t)(c & 1) * PB_STAGE;
+    const int nw = chunk_words(c);
+#pragma unroll
+    for (int w = 0; w < PB_WC; ++w) {
+      if (w < nw) {  // wave-uniform
+        const double2 a0 = buf[((2 * rp) * PB_WC + w) * 64 + lane];
+        const double2 a1 = buf[((2 * rp + 1) * PB_WC + w) * 64 + lane];
+        const double2 b0 = buf[((PB_RT + 2 * cp) * PB_WC + w) * 64 + lane];
+        const double2 b1 = buf[((PB_RT + 2 * cp + 1) * PB_WC + w) * 64 + lane];
+        constexpr int ch0 = 0;
+        const int chx = ch0 + 2 * (w & 1);  // compile-time after unrolling: k-block 2 j (+1) of the half
+        acc[0][0][chx] = mfma_f64(a0.x, b0.x, acc[0][0][chx]);
+        acc[0][1][chx] = mfma_f64(a0.x, b1.x, acc[0][1][chx]);
+        acc[1][0][chx] = mfma_f64(a1.x, b0.x, acc[1][0][chx]);
+        acc[1][1][chx] = mfma_f64(a1.x, b1.x, acc[1][1][chx]);
+        acc[0][0][chx + 1] = mfma_f64(a0.y, b0.y, acc[0][0][chx + 1]);
+        acc[0][1][chx + 1] = mfma_f64(a0.y, b1.y, acc[0][1][chx + 1]);
+        acc[1][0][chx + 1] = mfma_f64(a1.y, b0.y, acc[1][0][chx + 1]);
+        acc[1][1][chx + 1] = mfma_f64(a1.y, b1.y, acc[1][1][chx + 1]);
+        if (want_var) {
+          qsq[0] = fma(a0.x, a0.x, qsq[0]);
+          qsq[0] = fma(a0.y, a0.y, qsq[0]);
+          qsq[1] = fma(a1.x, a1.x, qsq[1]);
+          qsq[1] = fma(a1.y, a1.y, qsq[1]);
+        }
+      }
+    }
+  }
+  KST(st, 3);
+  // epilogue: s k(x_b, D_k) - (half 0 + half 1), the coincidence marks and the variances
+  const double os = o.outputscale;
+  const int kind = o.kernel;
+  const int rec = cov_rec(P->m);
+  d4 tot[2][2];  // half 0 + half 1 (the chains are dead from here: registers for the kernel terms)
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) tot[h][g] = sum0[h][g] + ((acc[h][g][0] + acc[h][g][1]) + (acc[h][g][2] + acc[h][g][3]));
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int k = 16 * (tk0 + 2 * cp + g) + (lane & 15);
+    const double* xk = P->disc + (size_t)min(k, N - 1) * d;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<double>(lane, r);
+        const double r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d);
+        const double kv = os * kernel_profile(kind, r2);
+        if (b < B && k < N) {
+          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kv - tot[h][g][r];
+          if (DKG_DUP_MARK && r2 == 0.0) atomicMin(&P->dup[b], k);  // Plan::dup
+        }
+      }
+    }
+  }
+  if (want_var) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double q = qsq[h];
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      const int bb = 16 * (ti0 + 2 * rp + h) + lane;
+      if (lane < 16 && bb < B) P->var[oi][bb] = os - (qh0[h] + q);
+    }
+  }
+  KST_END(st);
+}
+
 template <int DM, class T = double>
 __global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
                                                                          const double* __restrict__ xnew, int B,

@@ -101,7 +101,10 @@ def _fingerprint(obj):
         if obj.numel() <= _BY_VALUE_NUMEL and obj.device.type == "cpu":
             # hyperparameters (lengthscales, outputscale, noise, constant mean, Standardize buffers): by value,
             # since gpytorch's initialize() and constraint setters write them through .data, which does not
-            # bump the version counter
+            # bump the version counter.  Device-resident ones are fingerprinted by identity and version only
+            # (a by-value read would synchronise the device on every forward): after editing the
+            # hyperparameters of a model that lives on the GPU through .data / initialize(), call
+            # clear_state_cache() and DiscreteKnowledgeGradient.invalidate()
             return (id(obj), obj._version) + _small_values(obj)
         return (id(obj), obj._version)
     if isinstance(obj, ModelListGPState):  # flat, no recursion: this runs on every forward
@@ -119,6 +122,16 @@ def _fingerprint(obj):
                 parts.append(_fingerprint(tt))
         return tuple(parts)
     return id(obj)
+
+
+def _weights_fingerprint(w):
+    """The scalarisation weights by identity and version counter, and by value when they are a small host
+    tensor (an edit through ``.data`` does not bump the version counter).  A device-resident weights tensor
+    edited through ``.data`` is not seen (reading it back would cost a device synchronisation per forward):
+    assign a new tensor instead."""
+    if w.device.type == "cpu" and w.numel() <= 4096:
+        return (id(w), w._version) + _small_values(w)
+    return (id(w), w._version)
 
 
 # Device states of recently used (model, discretisation) pairs.  The reference builds one acquisition
@@ -263,12 +276,16 @@ class DiscreteKnowledgeGradient(_Base):
         self._device = device
         self._fp = _fingerprint(model)
         self._state = shared_state(state, self._fp, x_discretisation, device, owner=model)
-        self._W = scalarisation_weights.detach().to(self._state.device, torch.double).contiguous()
+        self._wfp = _weights_fingerprint(scalarisation_weights)
+        self._W = scalarisation_weights.detach().to(self._state.device, torch.double, copy=True).contiguous()
         self._plan = None
         self._plan_grad = None
 
     def _refresh(self):
-        """Rebuild the device state if the model changed since it was read (see _fingerprint)."""
+        """Rebuild the device state if the model changed since it was read (see _fingerprint), and the plans
+        if the scalarisation weights did: the reference reads both live at every forward (discretekg.py:
+        131-159, 182-185).  The plans hold a snapshot of the weights (their intercept caches are derived from
+        it), so an in-place edit of ``scalarisation_weights`` or a new tensor assigned to it is seen here."""
         fp = _fingerprint(self.model)
         if fp != self._fp:
             self._state = shared_state(_as_model_state(self.model), fp, self.x_discretisation, self._device,
@@ -276,6 +293,23 @@ class DiscreteKnowledgeGradient(_Base):
             self._plan = None
             self._plan_grad = None
             self._fp = fp
+        wfp = _weights_fingerprint(self.scalarisation_weights)
+        if wfp != self._wfp:
+            w = self.scalarisation_weights
+            if w.dim() != 2 or w.shape[-1] != self._W.shape[-1]:
+                raise BotorchTensorDimensionError(
+                    f"Expected 'scalarisation_weights' to stay S x {self._W.shape[-1]}. Got {tuple(w.shape)}.")
+            self._W = w.detach().to(self._state.device, torch.double, copy=True).contiguous()
+            self._plan = None
+            self._plan_grad = None
+            self._wfp = wfp
+
+    def invalidate(self) -> None:
+        """Re-read the model at the next forward whatever its fingerprint says (a device-resident model whose
+        hyperparameters were edited through ``.data``, which the fingerprint cannot see without a device
+        synchronisation per forward).  Also drops the shared device state built from the old values."""
+        clear_state_cache()
+        self._fp = None
 
     def _plan_for(self, B: int, grad: bool = False):
         """The forward plan (with gradient buffers when ``grad``), grown (powers of two) to hold B candidates."""

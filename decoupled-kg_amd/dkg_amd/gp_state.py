@@ -182,7 +182,9 @@ class ForwardPlan:
         lib = _lib.load()
         self.state = state
         self.device = state.device
-        self.W = W.detach().to(self.device, torch.double).contiguous()
+        # a snapshot: the plan's intercept cache and top hints (Plan::icpt / itop, built at init) are derived from
+        # these weights, so a caller editing its own weights tensor in place must not reach the plan's copy
+        self.W = W.detach().to(self.device, torch.double, copy=True).contiguous()
         if self.W.dim() != 2 or self.W.shape[1] != state.m:
             raise ValueError(f"weights must be S x {state.m}")
         self.S = self.W.shape[0]

@@ -163,7 +163,11 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
  * the plan is in use) and copies it to `dev_plan` (device memory of the same
  * size) on `stream`.  dkg_plan_forward then launches the three kernels with a
  * pointer to the device copy (no per-call host-to-device traffic).  The
- * disc/weights/workspace buffers must outlive the plan. */
+ * disc/weights/workspace buffers must outlive the plan.  The weights are
+ * frozen at dkg_plan_init: the staged envelope's intercept cache and each
+ * scalarisation's top intercept (Plan::icpt / itop) are derived from them
+ * there, so a caller that changes its weights builds a new plan (the Python
+ * host passes the plan a copy of its weights and rebuilds on a change). */
 /* Plan flags: DKG_PLAN_GRAD adds the gradient buffers (dkg_plan_forward_grad). */
 #define DKG_PLAN_GRAD 1
 /* DKG_PLAN_FORCE_WALK (test hook): the envelope stage takes its list-overflow
@@ -318,7 +322,8 @@ int dkg_debug_mfma_f64(const double* a, const double* b, double* c, void* stream
  * stream's graphs in turn leaves the last stream idle for the others' launches.  The
  * launcher keeps `threads - 1` worker threads (the caller is thread 0); stream s's graphs
  * graphs[offs[s] .. offs[s+1]) (hipGraphExec_t) are launched in order on streams[s] (hipStream_t) by
- * thread s % threads.  dkg_launcher_graphs returns once every launch call has returned.  Armed
+ * thread s % threads.  dkg_launcher_graphs returns once every launch call has returned; concurrent
+ * calls on one launcher are serialised (a launcher runs one launch set at a time).  Armed
  * workers spin (wake-up in ~1 us) for `seconds`; otherwise they sleep on a condition variable.
  * Host-side scheduling only (the reference has no counterpart: its forward is a Python loop,
  * discretekg.py:145-159); no kernel is launched that the caller did not capture. */

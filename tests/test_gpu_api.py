@@ -103,6 +103,41 @@ def test_model_is_read_live():
     assert acq._state is st
 
 
+@pytest.mark.parametrize("where", ["cpu", DEV])
+def test_weights_are_read_live(where):
+    """The scalarisation weights are read at every forward, as the reference's forward reads
+    self.scalarisation_weights: an in-place edit (host) or a newly assigned tensor (host or device) gives the
+    new weights' KG, while the plans keep their own snapshot (an edit never reaches a plan directly)."""
+    from helpers import assert_within, stated_tol
+    from oracle.discretekg import discrete_kg_batched, lines_batched
+    from oracle.gp import ModelList, OutputGP
+
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    om = ModelList([OutputGP(m.train_x, m.train_y, m.lengthscale, m.outputscale, m.noise, m.mean_constant,
+                             m.kernel, m.nu, m.y_mean, m.y_std) for m in model.models])
+    Xb = X[:8]
+    Wl = W.clone().to(where)
+    acq = DiscreteKnowledgeGradient(model, D, Wl)
+    base = acq(Xb.unsqueeze(-2)).cpu()
+    W2 = W.flip(-1).contiguous()
+    if where == "cpu":
+        Wl.data.copy_(W2)         # in place through .data (no version bump): seen by value
+    else:
+        acq.scalarisation_weights = W2.to(where)
+    got = acq(Xb.unsqueeze(-2)).cpu()
+    ref, _ = discrete_kg_batched(om, Xb, D, W2)
+    fresh = DiscreteKnowledgeGradient(model, D, W2)(Xb.unsqueeze(-2)).cpu()
+    assert torch.equal(got, fresh)
+    assert not torch.equal(got, base)
+    assert_within(got, ref, stated_tol(ref, lines_batched(om, Xb, D, W2)[0].abs().amax((-1, -2))))
+    # a plan's weights are its own copy: editing the tensor a plan was built from changes nothing in it
+    Wd = W.to(DEV)
+    plan = acq._state.plan(Wd, None, 8)
+    k1 = plan.forward(Xb.to(DEV)).cpu()
+    Wd.mul_(0.5)
+    assert torch.equal(plan.forward(Xb.to(DEV)).cpu(), k1)
+
+
 def test_single_output_model_without_weights():
     g = torch.Generator().manual_seed(2)
     Xt = torch.rand(30, 2, generator=g, dtype=torch.double)

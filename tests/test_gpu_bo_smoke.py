@@ -93,7 +93,7 @@ def test_smoke_pipeline_matches_the_oracle_run(seed, monkeypatch):
 
     The first BO step of both modes also matches the oracle run committed in tests/golden/smoke_oracle.json
     (make_smoke_oracle.py) at the optimiser's tolerance: L-BFGS-B stops at a relative decrease of 2.2e-9,
-    so |dx| ~ 1e-4.  Later steps are compared on the objective choice only.  The surrogates use noise 1e-8
+    so |dx| ~ 1e-4.  Later steps are compared on the objective choice and, loosely, on x and the value.  The surrogates use noise 1e-8
     (bo_loop.py:583-588), so their conditioning (~1e10 for the 1.8-lengthscale output) amplifies rounding
     in the observed values.  A rounding-level change of the device posterior mean moves the second full
     step's optimum by 5e-4 and its value by 1.5e-5 relative.  That sensitivity is in the problem, not in
@@ -143,4 +143,10 @@ def test_smoke_pipeline_matches_the_oracle_run(seed, monkeypatch):
         assert g["obj_index"] == w["obj_index"], mode
         assert g["x"][0] == pytest.approx(w["x"][0], abs=1e-4), (mode, g["x"][0], w["x"][0])
         assert g["acq"][0] == pytest.approx(w["acq"][0], rel=1e-6, abs=1e-8), mode
+        # later steps, loosely: the committed trajectory's conditioning moves a later optimum by ~5e-4 and its
+        # value by ~1.5e-5 relative under a rounding-level change of the posterior mean (above), so a drift of
+        # the device run away from the reference trajectory still shows at 2e-3 / 1e-4
+        for k in range(1, len(w["x"])):
+            assert g["x"][k] == pytest.approx(w["x"][k], abs=2e-3), (mode, k, g["x"][k], w["x"][k])
+            assert g["acq"][k] == pytest.approx(w["acq"][k], rel=1e-4, abs=1e-8), (mode, k)
         assert all(a > 0 for a in g["acq"])
