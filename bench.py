@@ -58,7 +58,7 @@ FP64_VALU_MEASURED_TFLOPS = 61.4
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 SIMDS, CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMDs
-PMC_DIR = os.path.join(REPO, "profiles", "r04")
+PMC_DIR = os.path.join(REPO, "profiles", "r05")
 
 
 def parse():
@@ -102,7 +102,7 @@ def parse():
                     help="timed steps of the non-degenerate headline-size leg (workload headline_nd; 0 = skip)")
     ap.add_argument("--pmc", default="auto",
                     help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py); auto: "
-                         "profiles/r04/pmc_<workload>[_fp32].json, none if that file does not exist")
+                         "profiles/r05/pmc_<workload>[_fp32].json, none if that file does not exist")
     ap.add_argument("--prep-reps", type=int, default=5, help="timed device-state preparations (0 = skip)")
     ap.add_argument("--stress-steps", type=int, default=8,
                     help="timed forwards of the stress leg (BASELINE configs[4] shape, fp64; 0 = skip)")
@@ -350,7 +350,9 @@ class Throughput:
         torch.cuda.synchronize()
         if graphs and graph == 2 and launcher is not None:
             launcher.arm(5.0 + 1e-4 * steps)  # workers spin through the timed region
+        # every event of the region made before its clock starts (creating one costs host time)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        evc = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record()
         if not graphs:
@@ -385,12 +387,13 @@ class Throughput:
                 host += time.perf_counter() - th
                 xchg.done(k0 + E - 1)
                 k0 += E
-        for k, g, u in self.chunks(k0, steps, G):
-            th = time.perf_counter()
-            unit(k, g, u)
-            host += time.perf_counter() - th
-        join()
-        evc = torch.cuda.Event(enable_timing=True)
+        if k0 < steps:  # steps past the last whole period (or no graphs): eager launches
+            for k, g, u in self.chunks(k0, steps, G):
+                th = time.perf_counter()
+                unit(k, g, u)
+                host += time.perf_counter() - th
+            join()
+        # (a whole-period region ended with every stream's join event on the main stream: no join needed)
         evc.record()  # every forward of the timed region enqueued before this point on the main stream
         xchg.flush(steps)
         ev1.record()
@@ -453,13 +456,18 @@ def batch_stats(plan, Xd):
             "kg_quantiles": {str(q): float(torch.quantile(kg_c, q)) for q in (0.0, 0.1, 0.5, 0.9, 1.0)}}
 
 
-def stage_rooflines(plan, Xd, model_fb, reps, precision, pmc):
-    """Every forward kernel against the compute roof (fp64 78.6 TF/s; the fp32 MFMA peak for fp32
-    contractions) with its counted flops, and against HBM with its algorithmic bytes.  Durations: HIP
-    events around `reps` back-to-back launches of the kernel alone on its own stream (dkg_plan_time_stage).
-    VALU-busy and traffic come from the workload's PMC file when there is one (else null)."""
+def stage_rooflines(plan, Xd, model_fb, reps, precision, pmc, G=1, B=None):
+    """Every forward kernel, as the timed region launches it (G forward batches of B candidates per launch:
+    ``plan`` holds G * B, ``Xd`` the G batches), against the compute roof (fp64 78.6 TF/s; the fp32 MFMA peak
+    for fp32 contractions) with its counted flops, and against HBM with its algorithmic bytes (``model_fb``:
+    stage_model of the whole launch).  Durations: HIP events around `reps` back-to-back launches of the
+    kernel alone on its own stream (dkg_plan_time_stage_batches).  VALU-busy and traffic come from the
+    workload's PMC file when there is one (else null)."""
     names = ["cross_root_kernel", "posterior_cov_kernel", "envelope_kernel"]
-    avg_ms = [plan.time_stage(Xd, k, reps) for k in range(3)]
+    if G > 1:
+        avg_ms = [plan.time_stage_batches(Xd, B, k, reps) for k in range(3)]
+    else:
+        avg_ms = [plan.time_stage(Xd, k, reps) for k in range(3)]
     out = {}
     for i, name in enumerate(names):
         fl, by = model_fb[name]
@@ -577,8 +585,12 @@ def main():
             pmc = json.load(open(pmc_path))
         except (OSError, ValueError):
             pmc = {}
-    model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], w.B, w.S, w.d)
-    stages = stage_rooflines(tp.plan, tp.Xd, model_fb, args.profile_reps, args.precision, pmc)
+    # the stages as the timed region launches them: G batches per launch
+    G = tp.G
+    model_fb = stage_model(w, w.m, [mm.num_train for mm in model.models], D.shape[0], G * w.B, w.S, w.d)
+    gplan_roof = acq._state.plan(acq._W, acq._target, G * w.B, f32=args.precision == "fp32")
+    stages = stage_rooflines(gplan_roof, tp.XG, model_fb, args.profile_reps, args.precision, pmc, G=G, B=w.B)
+    del gplan_roof
     dom = max(stages, key=lambda k: stages[k]["avg_launch_us"])
     roof = dict(stages[dom], kernel=dom,
                 bound_note="fp64 compute roof: 78.6 TF/s is both the vector and the matrix fp64 peak of MI355X; "
@@ -587,6 +599,7 @@ def main():
                            "flops): valu_busy_frac is its occupancy figure",
                 stages={k: {kk: v[kk] for kk in ("avg_launch_us", "bound", "frac", "valu_busy_frac", "traffic")}
                         for k, v in stages.items()},
+                launch=f"{G} forward batch(es) of {w.B} candidates per launch, as in the timed region",
                 pmc_source=os.path.relpath(pmc_path, REPO) if pmc else None)
 
     # ---- whole-forward roofline as BASELINE.md defines it: max(F/P, Bytes/BW) / T_measured
@@ -706,7 +719,7 @@ def main():
         ws, ms, Ds, _, _, _, tps = setup("stress", G=1)
         es = tps.run(1, args.stress_steps, 2, False, world)
         fb = stage_model(ws, ws.m, [mm.num_train for mm in ms.models], Ds.shape[0], ws.B, ws.S, ws.d)
-        # the stress workload's own PMC file (profiles/r04/pmc_stress.json) for its stages' traffic / busy figures
+        # the stress workload's own PMC file (profiles/r05/pmc_stress.json) for its stages' traffic / busy figures
         pmc_s_path = os.path.join(PMC_DIR, "pmc_stress.json")
         pmc_s = json.load(open(pmc_s_path)) if os.path.exists(pmc_s_path) else {}
         st_s = stage_rooflines(tps.plan, tps.Xd, fb, 3, "fp64", pmc_s)

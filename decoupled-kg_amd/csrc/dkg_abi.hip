@@ -530,8 +530,8 @@ int dkg_forward_timed(const dkg_output* outs, int m, int d, const double* disc, 
 
 size_t dkg_plan_bytes(void) { return sizeof(Plan); }
 
-int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
-                        double* kg_pairs, void* stream, int stage, int reps, float* avg_ms) {
+static int time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                      double* kg_pairs, void* stream, int stage, int reps, float* avg_ms, int geom_B) {
   if (!host_plan || !dev_plan || !avg_ms) return fail(DKG_ERR_ARG, "NULL pointer");
   if (stage < 0 || stage > 3 || reps < 1) return fail(DKG_ERR_ARG, "stage=%d reps=%d", stage, reps);
   const Plan& h = *static_cast<const Plan*>(host_plan);
@@ -544,11 +544,12 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
   for (int k = 0; k < 2; ++k)
     if ((st = hip_check(hipEventCreate(&ev[k]), "hipEventCreate"))) return st;
   // prime the inputs of the timed stage, then time reps back-to-back launches of it alone
-  if ((st = hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr), "forward"))) return st;
+  if ((st = hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr, geom_B), "forward"))) return st;
   (void)hipEventRecord(ev[0], s);
   for (int r = 0; r < reps; ++r)
-    if ((st = hip_check(stage == 3 ? launch_forward_auto(h, dev, xnew, B, kg, nullptr, s)
-                                   : launch_stage(h, dev, xnew, B, kg, kg_pairs, s, stage),
+    if ((st = hip_check(stage == 3 ? (geom_B ? launch_forward(h, dev, xnew, B, kg, nullptr, s, nullptr, geom_B)
+                                             : launch_forward_auto(h, dev, xnew, B, kg, nullptr, s))
+                                   : launch_stage(h, dev, xnew, B, kg, kg_pairs, s, stage, geom_B),
                         "stage")))
       return st;
   (void)hipEventRecord(ev[1], s);
@@ -558,7 +559,18 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
   *avg_ms = ms / reps;
   for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev[k]);
   // leave kg / kg_pairs valid again (repeated stages accumulate into kg)
-  return hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr), "forward");
+  return hip_check(launch_forward(h, dev, xnew, B, kg, kg_pairs, s, nullptr, geom_B), "forward");
+}
+
+int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
+                        double* kg_pairs, void* stream, int stage, int reps, float* avg_ms) {
+  return time_stage(host_plan, dev_plan, xnew, B, kg, kg_pairs, stream, stage, reps, avg_ms, 0);
+}
+
+int dkg_plan_time_stage_batches(const void* host_plan, const void* dev_plan, const double* xnew, int B, int nbatch,
+                                double* kg, void* stream, int stage, int reps, float* avg_ms) {
+  if (B < 1 || nbatch < 1) return fail(DKG_ERR_ARG, "B=%d nbatch=%d", B, nbatch);
+  return time_stage(host_plan, dev_plan, xnew, B * nbatch, kg, nullptr, stream, stage, reps, avg_ms, B);
 }
 
 size_t dkg_plan_workspace(const dkg_output* outs, int m, int d, int N, int max_B, int S, int flags) {

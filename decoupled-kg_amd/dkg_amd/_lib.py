@@ -85,6 +85,8 @@ SIGNATURES = {
                                        POINTER(c_float)]),
     "dkg_plan_time_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                     c_int, POINTER(c_float)]),
+    "dkg_plan_time_stage_batches": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                                            c_int, POINTER(c_float)]),
     "dkg_plan_hull_sizes": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "dkg_plan_status": (c_int, [c_void_p, POINTER(c_int), c_int, c_void_p]),
     "dkg_plan_fused": (c_int, [c_void_p]),

@@ -428,6 +428,18 @@ class ForwardPlan:
                                                    ctypes.byref(ms)), "dkg_plan_time_stage")
         return ms.value
 
+    def time_stage_batches(self, X: torch.Tensor, B: int, stage: int, reps: int) -> float:
+        """time_stage for the launches of ``forward_batches_into`` (X: K*B candidates, K batches of B)."""
+        X = X.detach().to(self.device, torch.double).contiguous()
+        if B < 1 or X.shape[0] % B:
+            raise ValueError(f"{X.shape[0]} candidates are not whole batches of {B}")
+        kg = torch.empty(X.shape[0], dtype=torch.double, device=self.device)
+        ms = _lib.c_float()
+        _lib.check(_lib.load().dkg_plan_time_stage_batches(self.host, self._dev_ptr, _lib.ptr(X), B, X.shape[0] // B,
+                                                           _lib.ptr(kg), current_stream_ptr(self.device), stage,
+                                                           reps, ctypes.byref(ms)), "dkg_plan_time_stage_batches")
+        return ms.value
+
     def forward(self, X: torch.Tensor, kg_pairs=None, timed: bool = False):
         X = X.detach().to(self.device, torch.double).contiguous()
         B = X.shape[0]

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DKG_ABI_VERSION 8  /* 8: dkg_plan_forward_batches; 7: plan flag DKG_PLAN_NO_CHAIN */
+#define DKG_ABI_VERSION 8  /* 8: dkg_plan_forward_batches, dkg_plan_time_stage_batches; 7: DKG_PLAN_NO_CHAIN */
 #define DKG_MAX_OUTPUTS 8   /* outputs (objectives) per model list */
 #define DKG_MAX_DIM 16      /* input dimension d */
 
@@ -261,6 +261,10 @@ int dkg_plan_fused(const void* host_plan);
  * forward leaves kg / kg_pairs valid.  Synchronises. */
 int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* kg,
                         double* kg_pairs, void* stream, int stage, int reps, float* avg_ms);
+/* As dkg_plan_time_stage for the launches of dkg_plan_forward_batches (nbatch batches of B candidates,
+ * xnew [nbatch][B][d], kg [nbatch][B]): the stage as that entry launches it (stage 3: its three kernels). */
+int dkg_plan_time_stage_batches(const void* host_plan, const void* dev_plan, const double* xnew, int B, int nbatch,
+                                double* kg, void* stream, int stage, int reps, float* avg_ms);
 
 /* Envelope stage alone: for P independent sets of L lines a_k + b_k z
  * (device, row-major [P][L]) kg[p] = E[max_k (a_k + b_k Z)] - max_k a_k, Z ~ N(0,1),

@@ -19,34 +19,62 @@ import sys
 
 KERNELS = {"cross_root_plan_kernel": "cross_root_kernel", "cross_kfill_kernel": "cross_kfill_kernel",
            "posterior_cov_kernel": "posterior_cov_kernel", "posterior_cov_wide_kernel": "posterior_cov_wide_kernel",
-           "envelope_kernel": "envelope_kernel"}
-# bench.py's stages: the kernels one forward launches per stage (large n: the K(x, X) fill before the cross
-# kernel; large B x N: the 64 x 64 covariance blocks), summed per forward
+           "posterior_cov_big_kernel": "posterior_cov_big_kernel", "envelope_kernel": "envelope_kernel"}
+# bench.py's stages: the kernels one launch of the timed region runs per stage (large n or many candidates:
+# the K(x, X) fill before the cross kernel; large B x N: the 64 x 64 or LDS-staged 64 x 128 covariance
+# blocks), summed per launch
 STAGES = {"cross_root_kernel": ("cross_root_kernel", "cross_kfill_kernel"),
-          "posterior_cov_kernel": ("posterior_cov_kernel", "posterior_cov_wide_kernel"),
+          "posterior_cov_kernel": ("posterior_cov_kernel", "posterior_cov_wide_kernel", "posterior_cov_big_kernel"),
           "envelope_kernel": ("envelope_kernel",)}
+
+
+def _name(kn):
+    for k, name in KERNELS.items():
+        if k in kn and not (k == "envelope_kernel" and ", true," in kn):
+            return name
+    return None
+
+
+def _grid(r):
+    if "Grid_Size" in r and r["Grid_Size"]:
+        return int(float(r["Grid_Size"]))
+    return int(float(r.get("Grid_Size_X") or 0)) * int(float(r.get("Grid_Size_Y") or 1)) * int(
+        float(r.get("Grid_Size_Z") or 1))
 CLOCK_GHZ = 2.4
 SIMDS = 1024
 
 
 def load(out):
-    agg = {}
+    """Per kernel, the counters of its dispatches of the largest grid (the timed region's launch shape: the
+    bench's diagnostics also launch single 128-candidate forwards), averaged per dispatch."""
+    rows = {}
     for f in glob.glob(f"{out}/*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            kn = r["Kernel_Name"]
-            for k, name in KERNELS.items():
-                if k in kn and not (k == "envelope_kernel" and ", true," in kn):
-                    agg.setdefault(name, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            name = _name(r["Kernel_Name"])
+            if name:
+                rows.setdefault(name, []).append((_grid(r), r["Counter_Name"], float(r["Counter_Value"])))
+    agg = {}
+    for name, rs in rows.items():
+        gmax = max(g for g, _, _ in rs)
+        for g, c, v in rs:
+            if g == gmax:
+                agg.setdefault(name, {}).setdefault(c, []).append(v)
     return {n: {c: sum(v) / len(v) for c, v in d.items()} for n, d in agg.items()}
 
 
 def durations(out):
-    d = {}
-    for f in glob.glob(f"{out}/trace/**/*kernel_stats.csv", recursive=True):
+    """Per kernel, the mean duration of its dispatches of the largest grid in the kernel trace."""
+    rows = {}
+    for f in glob.glob(f"{out}/trace/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            for k, name in KERNELS.items():
-                if k in r["Name"] and not (k == "envelope_kernel" and ", true," in r["Name"]):
-                    d[name] = float(r["AverageNs"]) / 1e3
+            name = _name(r["Kernel_Name"])
+            if name:
+                rows.setdefault(name, []).append((_grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    d = {}
+    for name, rs in rows.items():
+        gmax = max(g for g, _ in rs)
+        v = [t for g, t in rs if g == gmax]
+        d[name] = sum(v) / len(v)
     return d
 
 
