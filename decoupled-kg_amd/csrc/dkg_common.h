@@ -185,6 +185,54 @@ __device__ __forceinline__ double kernel_profile_t(double r2, const_dptr tab = p
   }
 }
 
+// The covariance stage's kernel terms: kernel_profile_t's expression compiled without FP contraction, every
+// product rounded on its own, so a term has the same bits in every kernel and context that evaluates it (the
+// covariance kernels' block shapes are bit-identical only if their terms are; left to the compiler, the same
+// expression was fused differently in two kernels).  exp_nonpos and sqrt_nonneg take their products through
+// explicit fma()s or contraction-free copies here.
+__device__ __forceinline__ double exp_nonpos_nc(double y, const_dptr tab) {
+#pragma clang fp contract(off)
+  y = (y < -760.0) ? -760.0 : y;
+  const double k = rint(y * 1.4426950408889634);
+  double r = fma(-k, 0.6931471805599453, y);
+  r = fma(-k, 2.3190468138462996e-17, r);
+  return ldexp(horner<14>(tab + PSI_OFF_EXP, r), (int)k);
+}
+__device__ __forceinline__ double sqrt_nonneg_nc(double x) {
+#pragma clang fp contract(off)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-g, h, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  const double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return (x > 0.0) ? g : 0.0;
+}
+template <int KIND>
+__device__ __forceinline__ double kernel_term_nc(double r2, const_dptr tab) {
+#pragma clang fp contract(off)
+  if constexpr (KIND == DKG_RBF) {
+    return exp_nonpos_nc(-0.5 * r2, tab);
+  } else if constexpr (KIND == DKG_MATERN12) {
+    return exp_nonpos_nc(-sqrt_nonneg_nc(r2), tab);
+  } else if constexpr (KIND == DKG_MATERN32) {
+    const double t = 1.7320508075688772 * sqrt_nonneg_nc(r2);
+    return (t + 1.0) * exp_nonpos_nc(-t, tab);
+  } else {
+    const double t = 2.23606797749979 * sqrt_nonneg_nc(r2);
+    return (t + 1.0 + (5.0 / 3.0) * r2) * exp_nonpos_nc(-t, tab);
+  }
+}
+__device__ __forceinline__ double kernel_term_nc(int kind, double r2, const_dptr tab) {
+  switch (kind) {
+    case DKG_RBF: return kernel_term_nc<DKG_RBF>(r2, tab);
+    case DKG_MATERN12: return kernel_term_nc<DKG_MATERN12>(r2, tab);
+    case DKG_MATERN32: return kernel_term_nc<DKG_MATERN32>(r2, tab);
+    default: return kernel_term_nc<DKG_MATERN52>(r2, tab);
+  }
+}
+
 // h(r2) = kappa'(r) / r of the kernel profile, so that for the scaled
 // difference t = (x - z) / l:  d[s kappa(|t|)]/dx_j = s h(|t|^2) t_j / l_j.
 // Finite at r = 0 except Matern-1/2, whose gradient at a coincident point is

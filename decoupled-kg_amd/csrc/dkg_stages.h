@@ -487,7 +487,9 @@ __device__ __forceinline__ void posterior_cov_body(const Plan* __restrict__ P, c
         const int b = ti * 16 + mfma_drow<T>(lane, rr);
         r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, disc_row(), o.inv_lengthscale, d);
       }
-      kv[rr] = os * kernel_profile(kind, r2, EPI_FIRST ? tab : psi_tab());
+      kv[rr] = os * kernel_term_nc(kind, r2, EPI_FIRST ? tab : psi_tab());
+      // rounded here, never fused into the epilogue's subtraction: posterior_cov_big_kernel gives the same bits
+      asm("" : "+v"(kv[rr]));
       if (DKG_DUP_MARK) hm[rr] = ballot(r2 == 0.0);
     }
   }
@@ -693,17 +695,27 @@ __global__ __launch_bounds__(PW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
 // (c0 + c1) + (c2 + c3), then half 0 + half 1; its variance sums likewise per half (lane-wise FMAs in k order,
 // then the xor-16 / xor-32 exchange), half 0 + half 1.  At 32 x 32 blocks every 16-byte operand load feeds two
 // MFMAs and the L1 path, not the MFMA, sets the rate once a launch fills the device (37 % of the fp64 roof
-// at 20 headline batches).  Here a workgroup of 8 waves (2 per SIMD) owns a 64 x 128 block (4 candidate
-// tiles x 8 line tiles of one output); the operand tiles are staged once per workgroup through LDS by
-// LDS-DMA in chunks of PB_WC words (double-buffered, the next chunk in flight during the current one's
-// MFMAs), and each wave computes a 2 x 2 group of tiles over both halves in turn (16 accumulator chains),
+// at 20 headline batches).  Here a workgroup of 4 waves (one per SIMD; two workgroups per CU, so one's
+// epilogue and chunk barriers overlap the other's MFMAs) owns a 64 x 64 block (4 candidate tiles x 4 line
+// tiles of one output); the operand tiles are staged once per workgroup through LDS in
+// chunks of PB_WC words by LDS-DMA (PB_NSTG buffers: three chunks in flight during the current one's MFMAs),
+// and each wave computes a 2 x 2 group of tiles over both halves in turn (16 accumulator chains),
 // reading its fragments from LDS with one 16-byte read per two MFMAs per operand tile.
-constexpr int PB_WAVES = 8;
+// 16 bytes from global memory by a global_load (address space 1), not a flat load.
+__device__ __forceinline__ double2 gload_d2(const double* p) {
+  typedef double v2 __attribute__((ext_vector_type(2)));
+  const v2 v = *reinterpret_cast<const __attribute__((address_space(1))) v2*>(reinterpret_cast<uintptr_t>(p));
+  return make_double2(v.x, v.y);
+}
+
+constexpr int PB_WAVES = 4;
 constexpr int PB_RT = 4;  // candidate tiles per block
-constexpr int PB_CT = 8;  // line tiles per block
-constexpr int PB_WC = 4;  // words (two k-blocks each) per staged chunk; even, so chains restart in step
+constexpr int PB_CT = 4;  // line tiles per block
+constexpr int PB_WC = 2;  // words (two k-blocks each) per staged chunk; even, so chains restart in step
 constexpr int PB_STAGE = (PB_RT + PB_CT) * PB_WC * 64;  // 16-byte words per stage buffer
-constexpr size_t PB_LDS = 2 * (size_t)PB_STAGE * 16;     // double-buffered: 96 KiB
+constexpr int PB_NSTG = 2;                               // stage buffers: chunks in flight + the one computed
+// the stage buffers, then the kernel terms (16 per lane per wave): 64 KiB, two workgroups per CU
+constexpr size_t PB_LDS = PB_NSTG * (size_t)PB_STAGE * 16 + (size_t)PB_WAVES * 16 * 64 * 8;
 
 template <int DM>
 __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_big_kernel(
@@ -731,13 +743,20 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   const int nc0 = (KPs + PB_WC - 1) / PB_WC, nc = nc0 + (KP - KPs + PB_WC - 1) / PB_WC;
   auto chunk_start = [&](int c) { return c < nc0 ? c * PB_WC : KPs + (c - nc0) * PB_WC; };
   auto chunk_words = [&](int c) { return c < nc0 ? min(PB_WC, KPs - c * PB_WC) : min(PB_WC, KP - chunk_start(c)); };
-  // chunk c's words of the block's tiles into buffer c & 1 (tiles past the matrix read its last tile: discarded)
+  // Chunk staging by LDS-DMA, PB_NSTG buffers deep: chunk c + PB_NSTG - 1 is in flight while chunk c is
+  // computed.  The fragment reads are inline-asm ds_reads with their own lgkmcnt waits: a compiler-visible
+  // LDS read after an LDS-DMA makes the compiler wait for every DMA in flight first (it cannot tell the
+  // buffers apart).  Every wave issues PB_PIECES DMA instructions per chunk (words past a chunk's end repeat
+  // a live word, unused), so the chunk-c wait is vmcnt <= PB_PIECES x (chunks issued after it).
+  constexpr int PB_PIECES = (PB_RT + PB_CT) * PB_WC / PB_WAVES;
+  static_assert((PB_RT + PB_CT) * PB_WC % PB_WAVES == 0 && PB_PIECES == 4, "four DMA pieces per wave per chunk");
   auto stage = [&](int c) {
     const int j0 = chunk_start(c), nw = chunk_words(c);
-    double2* buf = stg + (size_t)(c & 1) * PB_STAGE;
-    for (int piece = wave; piece < (PB_RT + PB_CT) * PB_WC; piece += PB_WAVES) {
-      const int t = piece / PB_WC, w = piece % PB_WC;
-      if (w >= nw) continue;  // wave-uniform
+    double2* buf = stg + (size_t)(c % PB_NSTG) * PB_STAGE;
+#pragma unroll
+    for (int q = 0; q < PB_PIECES; ++q) {
+      const int piece = wave + PB_WAVES * q;
+      const int t = piece / PB_WC, w = min(piece % PB_WC, nw - 1);
       const double* src = t < PB_RT ? qx : qd;
       const int tile = t < PB_RT ? min(ti0 + t, RT - 1) : min(tk0 + t - PB_RT, CT - 1);
       __builtin_amdgcn_global_load_lds(
@@ -746,6 +765,11 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
           16, 0, 0);
     }
   };
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  // per-lane LDS byte addresses of the wave's candidate tiles (2 rp, 2 rp + 1) and line tiles in buffer 0
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
+  const uint32_t addrA = lds0 + (uint32_t)(((2 * rp) * PB_WC) * 64 + lane) * 16;
+  const uint32_t addrB = lds0 + (uint32_t)(((PB_RT + 2 * cp) * PB_WC) * 64 + lane) * 16;
   const bool want_var = bx == 0 && cp == 0;  // the wave's column tiles include tile 0: its row tiles' variances
   d4 acc[2][2][4];
 #pragma unroll
@@ -756,12 +780,77 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
       for (int c = 0; c < 4; ++c) acc[h][g][c] = d4{0.0, 0.0, 0.0, 0.0};
   d4 sum0[2][2];
   double qsq[2] = {0.0, 0.0}, qh0[2] = {0.0, 0.0};
-  stage(0);
+#pragma unroll
+  for (int c = 0; c < PB_NSTG - 1; ++c)
+    if (c < nc) stage(c);
+  // The kernel terms s k(x_b, D_k) of the wave's 16 elements per lane (scaled_r2_dm's and kernel_profile's
+  // arithmetic), evaluated while the first chunks' DMAs are in flight and parked in LDS (16 x 8 bytes per
+  // lane: in registers they would stay live across the contraction): the epilogue then only stores.
+  // r^2 == 0 (Plan::dup) as one bit per element.
+  const double os = o.outputscale;
+  double* kvs = reinterpret_cast<double*>(stg + (size_t)PB_NSTG * PB_STAGE) + (size_t)wave * 16 * 64;
+  uint32_t zero_r2 = 0;
+  {
+    const int kind = o.kernel;
+    const double* __restrict__ il_p = o.inv_lengthscale;
+    const double* __restrict__ disc = P->disc;
+    double il[DM], xkv[2][DM];
+#pragma unroll
+    for (int c = 0; c < DM; ++c) il[c] = il_p[min(c, d - 1)];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int k = 16 * (tk0 + 2 * cp + g) + (lane & 15);
+#pragma unroll
+      for (int c = 0; c < DM; ++c) xkv[g][c] = disc[(size_t)min(k, N - 1) * d + min(c, d - 1)];
+    }
+    // one covariance family per instantiation (the switch outside the 16 terms: straight-line code the
+    // scheduler interleaves) and one coefficient-table pointer for all of them.  kernel_term_nc is compiled
+    // without FP contraction (dkg_common.h), so the terms are posterior_cov_body's bits.
+    auto terms = [&](auto kind_c) __attribute__((always_inline)) {
+      constexpr int KIND = decltype(kind_c)::value;
+      const const_dptr tab = psi_tab();
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<double>(lane, r);
+          double xb[DM];
+#pragma unroll
+          for (int c = 0; c < DM; ++c) xb[c] = xnew[(size_t)min(b, B - 1) * d + min(c, d - 1)];
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            double r2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < DM; ++c) {
+              const double t = (xb[c] - xkv[g][c]) * il[c];
+              r2 = fma(t, (c < d) ? t : 0.0, r2);
+            }
+            const double kv = os * kernel_term_nc<KIND>(r2, tab);  // rounded (stored), as posterior_cov_body
+            const int e = (g * 2 + h) * 4 + r;
+            kvs[e * 64 + lane] = kv;
+            zero_r2 |= (r2 == 0.0 ? 1u : 0u) << e;
+          }
+        }
+    };
+    switch (kind) {
+      case DKG_MATERN12: terms(std::integral_constant<int, DKG_MATERN12>{}); break;
+      case DKG_MATERN32: terms(std::integral_constant<int, DKG_MATERN32>{}); break;
+      case DKG_RBF: terms(std::integral_constant<int, DKG_RBF>{}); break;
+      default: terms(std::integral_constant<int, DKG_MATERN52>{}); break;
+    }
+  }
   KST(st, 2);
   for (int c = 0; c < nc; ++c) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // chunk c landed; every wave is done with the other buffer
-    if (c + 1 < nc) stage(c + 1);
+    // chunk c landed (this wave's pieces), then every wave's: the later chunks' DMAs stay in flight
+    const int later = min(nc - 1 - c, PB_NSTG - 2);  // chunks issued after c (wave-uniform)
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // a bare s_barrier: __syncthreads()'s workgroup fence would make the compiler drain every DMA in flight
+    // (vmcnt(0)) first; LDS needs no fence within the workgroup once the DMA has landed (vmcnt above)
+    asm volatile("s_barrier" ::: "memory");
+    // buffer (c + PB_NSTG - 1) % PB_NSTG held chunk c - 1, which every wave finished before the barrier
+    if (c + PB_NSTG - 1 < nc) stage(c + PB_NSTG - 1);
     if (c == nc0) {  // half 0 done: its sums, and the chains restart for half 1
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -782,61 +871,84 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
         }
       }
     }
-    const double2* buf = stg + (size_t)(c & 1) * PB_STAGE;
+    const uint32_t so = (uint32_t)(c % PB_NSTG) * (uint32_t)(PB_STAGE * 16);
+    const uint32_t aA = addrA + so, aB = addrB + so;
     const int nw = chunk_words(c);
-#pragma unroll
-    for (int w = 0; w < PB_WC; ++w) {
-      if (w < nw) {  // wave-uniform
-        const double2 a0 = buf[((2 * rp) * PB_WC + w) * 64 + lane];
-        const double2 a1 = buf[((2 * rp + 1) * PB_WC + w) * 64 + lane];
-        const double2 b0 = buf[((PB_RT + 2 * cp) * PB_WC + w) * 64 + lane];
-        const double2 b1 = buf[((PB_RT + 2 * cp + 1) * PB_WC + w) * 64 + lane];
-        constexpr int ch0 = 0;
-        const int chx = ch0 + 2 * (w & 1);  // compile-time after unrolling: k-block 2 j (+1) of the half
-        acc[0][0][chx] = mfma_f64(a0.x, b0.x, acc[0][0][chx]);
-        acc[0][1][chx] = mfma_f64(a0.x, b1.x, acc[0][1][chx]);
-        acc[1][0][chx] = mfma_f64(a1.x, b0.x, acc[1][0][chx]);
-        acc[1][1][chx] = mfma_f64(a1.x, b1.x, acc[1][1][chx]);
-        acc[0][0][chx + 1] = mfma_f64(a0.y, b0.y, acc[0][0][chx + 1]);
-        acc[0][1][chx + 1] = mfma_f64(a0.y, b1.y, acc[0][1][chx + 1]);
-        acc[1][0][chx + 1] = mfma_f64(a1.y, b0.y, acc[1][0][chx + 1]);
-        acc[1][1][chx + 1] = mfma_f64(a1.y, b1.y, acc[1][1][chx + 1]);
-        if (want_var) {
-          qsq[0] = fma(a0.x, a0.x, qsq[0]);
-          qsq[0] = fma(a0.y, a0.y, qsq[0]);
-          qsq[1] = fma(a1.x, a1.x, qsq[1]);
-          qsq[1] = fma(a1.y, a1.y, qsq[1]);
-        }
+    // the chunk's two words in two register sets (no copies between them: a VALU copy into registers an
+    // MFMA group just read holds the next group until that group has read them): word 1's read is issued
+    // before word 0's MFMAs, and LDS reads complete in order, so lgkmcnt(4) means word 0 has landed
+    static_assert(PB_WC == 2, "two words per chunk: register sets X and Y");
+    v2d xa0, xa1, xb0, xb1, ya0, ya1, yb0, yb1;
+    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:%6\n\tds_read_b128 %2, %5\n\t"
+                 "ds_read_b128 %3, %5 offset:%6"
+                 : "=&v"(xa0), "=&v"(xa1), "=&v"(xb0), "=&v"(xb1)
+                 : "v"(aA), "v"(aB), "i"(PB_WC * 1024)
+                 : "memory");
+    const bool two = nw > 1;  // wave-uniform
+    if (two) {
+      asm volatile("ds_read_b128 %0, %4 offset:1024\n\tds_read_b128 %1, %4 offset:%6\n\t"
+                   "ds_read_b128 %2, %5 offset:1024\n\tds_read_b128 %3, %5 offset:%6"
+                   : "=&v"(ya0), "=&v"(ya1), "=&v"(yb0), "=&v"(yb1)
+                   : "v"(aA), "v"(aB), "i"((PB_WC + 1) * 1024)
+                   : "memory");
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
+    }
+    auto word = [&](const v2d& a0, const v2d& a1, const v2d& b0, const v2d& b1, auto chc) __attribute__((always_inline)) {
+      constexpr int chx = decltype(chc)::value;  // k-blocks 2 j, 2 j + 1 of the half: chains chx, chx + 1
+      acc[0][0][chx] = mfma_f64(a0.x, b0.x, acc[0][0][chx]);
+      acc[0][1][chx] = mfma_f64(a0.x, b1.x, acc[0][1][chx]);
+      acc[1][0][chx] = mfma_f64(a1.x, b0.x, acc[1][0][chx]);
+      acc[1][1][chx] = mfma_f64(a1.x, b1.x, acc[1][1][chx]);
+      acc[0][0][chx + 1] = mfma_f64(a0.y, b0.y, acc[0][0][chx + 1]);
+      acc[0][1][chx + 1] = mfma_f64(a0.y, b1.y, acc[0][1][chx + 1]);
+      acc[1][0][chx + 1] = mfma_f64(a1.y, b0.y, acc[1][0][chx + 1]);
+      acc[1][1][chx + 1] = mfma_f64(a1.y, b1.y, acc[1][1][chx + 1]);
+      if (want_var) {
+        qsq[0] = fma(a0.x, a0.x, qsq[0]);
+        qsq[0] = fma(a0.y, a0.y, qsq[0]);
+        qsq[1] = fma(a1.x, a1.x, qsq[1]);
+        qsq[1] = fma(a1.y, a1.y, qsq[1]);
       }
+    };
+    word(xa0, xa1, xb0, xb1, std::integral_constant<int, 0>{});
+    if (two) {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
+      word(ya0, ya1, yb0, yb1, std::integral_constant<int, 2>{});
     }
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   KST(st, 3);
   // epilogue: s k(x_b, D_k) - (half 0 + half 1), the coincidence marks and the variances
-  const double os = o.outputscale;
-  const int kind = o.kernel;
   const int rec = cov_rec(P->m);
   d4 tot[2][2];  // half 0 + half 1 (the chains are dead from here: registers for the kernel terms)
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int g = 0; g < 2; ++g) tot[h][g] = sum0[h][g] + ((acc[h][g][0] + acc[h][g][1]) + (acc[h][g][2] + acc[h][g][3]));
+    for (int g = 0; g < 2; ++g) {
+      tot[h][g] = sum0[h][g] + ((acc[h][g][0] + acc[h][g][1]) + (acc[h][g][2] + acc[h][g][3]));
+      asm volatile("" : "+v"(tot[h][g]));  // formed here: the chains are dead before the epilogue's loads
+    }
+  // the stores: the kernel terms from LDS (evaluated before the contraction), minus the contraction.  The
+  // lane index through an opaque copy: the store addresses are formed here, not hoisted across the loop
+  // (16 live 64-bit addresses spilled)
+  int le = lane;
+  asm volatile("" : "+v"(le));
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    const int k = 16 * (tk0 + 2 * cp + g) + (lane & 15);
-    const double* xk = P->disc + (size_t)min(k, N - 1) * d;
+    const int k = 16 * (tk0 + 2 * cp + g) + (le & 15);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<double>(lane, r);
-        const double r2 = scaled_r2_dm<DM>(xnew + (size_t)min(b, B - 1) * d, xk, o.inv_lengthscale, d);
-        const double kv = os * kernel_profile(kind, r2);
+        const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<double>(le, r);
+        const int e = (g * 2 + h) * 4 + r;
         if (b < B && k < N) {
-          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kv - tot[h][g][r];
-          if (DKG_DUP_MARK && r2 == 0.0) atomicMin(&P->dup[b], k);  // Plan::dup
+          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kvs[e * 64 + le] - tot[h][g][r];
+          if (DKG_DUP_MARK && ((zero_r2 >> e) & 1)) atomicMin(&P->dup[b], k);  // Plan::dup
         }
       }
-    }
   }
   if (want_var) {
 #pragma unroll
