@@ -61,7 +61,6 @@ struct WsLayout {
   size_t dup;
   size_t hull_pairs;
   size_t icpt, itop, itopk;  // 0: none (streaming envelope)
-  size_t wq, wqctl;          // split envelope queue
   size_t total;
 };
 
@@ -127,8 +126,8 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
   envelope_geometry(std::max(B, 1), std::max(S, 1), &sw, &split, !(flags & DKG_PLAN_FUSED));
   // split > 1: every pair's KG (and, value+gradient, its dKG/dx) for the last workgroup's ordered sums
   const size_t pcols = (size_t)std::max(S, 1) + pair_groups(std::max(S, 1));  // pair values + group terms
-  L.wg_part = off;  // (the split envelope's group rows too, at any split)
-  off = align256(off + (size_t)std::max(B, 1) * pcols * sizeof(double));
+  L.wg_part = off;
+  off = align256(off + (split > 1 ? (size_t)std::max(B, 1) * pcols * sizeof(double) : 0));
   L.wg_gpart = off;
   off = align256(off + ((flags & DKG_PLAN_GRAD) && split > 1 ? (size_t)std::max(B, 1) * pcols * d * sizeof(double) : 0));
   L.tickets = off;
@@ -145,10 +144,6 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
     L.itopk = off;
     off = align256(off + (size_t)std::max(S, 1) * 2 * sizeof(int));
   }
-  L.wq = off;
-  off = align256(off + (size_t)std::max(B, 1) * std::max(S, 1) * sizeof(int));
-  L.wqctl = off;
-  off = align256(off + 2 * sizeof(unsigned));
   L.total = off;
   return L;
 }
@@ -249,8 +244,6 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
   P->dup = reinterpret_cast<int*>(ws + L.dup);
   P->wg_gpart = reinterpret_cast<double*>(ws + L.wg_gpart);
   P->hull_pairs = reinterpret_cast<int*>(ws + L.hull_pairs);
-  P->wq = reinterpret_cast<int*>(ws + L.wq);
-  P->wqctl = reinterpret_cast<unsigned*>(ws + L.wqctl);
   // the intercept cache serves the staged forward envelope (a gradient plan's forward included)
   if (L.icpt && !stream) {
     P->icpt = reinterpret_cast<double*>(ws + L.icpt);

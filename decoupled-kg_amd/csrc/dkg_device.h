@@ -1505,14 +1505,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
                                               const double* __restrict__ mux_all, const double* __restrict__ wts,
                                               const int* __restrict__ dupv, long long cov_stride, int bpad, int b,
                                               int g, int G, double* smem, unsigned long long* st,
-                                              const Handoff* ho = nullptr, double* __restrict__ hout = nullptr,
-                                              int* __restrict__ wq = nullptr, unsigned* __restrict__ wqctl = nullptr) {
+                                              const Handoff* ho = nullptr, double* __restrict__ hout = nullptr) {
   static_assert(!HO || (!GRAD && !STREAM), "the fused forward stages its lines (no gradient, no streaming)");
-  // wq (split envelope, staged forward only): the pairs the flat test does not settle are queued (b S + j)
-  // for envelope_walk_kernel instead of walked here, and their groups' sums are left to it
-  constexpr bool SPLIT_OK = !GRAD && !STREAM && !HO;
-  __shared__ int s_nq;  // split envelope: this workgroup's queued pairs
-  if (SPLIT_OK && threadIdx.x == 0) s_nq = 0;
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space),
   // and line 0's inputs: the mean and slope component it is built from (x_b's own, or, when x_b coincides
   // with a discretisation point (Plan::dup), that line's record: line 0 is then its exact copy)
@@ -2463,24 +2457,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
           hint = TopHint{true, A1, bk};
         }
       }
-      if (SPLIT_OK && wq != nullptr) {
-        // split envelope: the lines and the flat test (env_pair_regs_edges' flat_ok steps, the same hint);
-        // a pair the test does not settle is queued, and envelope_walk_kernel runs env_pair_regs on it
-        double la[MAXL], lb[MAXL];
-        build_lines(la, lb);
-        FwdEnv fe;
-        if (hint.valid) {
-          fe.aT = hint.aT;
-          fe.bT = hint.bT;
-        } else {
-          env_top<MAXL>(la, lb, fe);
-        }
-        kgj = 0.0;  // flat: exactly 0 (env_flat); queued: written by envelope_walk_kernel
-        if (!env_flat<MAXL>(la, lb, fe) && lane == 0) {
-          wq[atomicAdd(&wqctl[0], 1u)] = b * S + j;
-          atomicAdd(&s_nq, 1);
-        }
-      } else if constexpr (ICP) {
+      if constexpr (ICP) {
         // intercepts from the plan (first build: the registers loaded ahead; a rebuild: global memory)
         auto slopes = [&](double (&lb)[MAXL]) {
           const double* cvr = lcv + (lane - 1) * MP;
@@ -2577,17 +2554,6 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
     int* tk = P->tickets + (size_t)b * (ng + 1); // [ng] group tickets, [ng] the candidate's
     __shared__ int s_last;
     const int dg = GRAD ? d : 0;
-    if (SPLIT_OK && wq != nullptr && s_nq > 0) {  // workgroup-uniform (s_nq read after the barrier above)
-      // the group's pair values (0 for the flat ones; the queued ones are overwritten) and its count of
-      // queued pairs: envelope_walk_kernel's last pair of the group sums it (a later kernel: plain stores)
-      if (threadIdx.x == 0) {
-        for (int q = 0; q < j1 - j0; ++q) P->wg_part[prow + j0 + q] = skg[q];
-        tk[grp] = s_nq;
-      }
-      if (st) __syncthreads();
-      KST_END(st);
-      return;
-    }
     // ---- level 1: G_g (thread 0) and, GRAD, its gradient (threads 1 .. d, one coordinate each)
     double gsum = 0.0;
     const int gi = (int)threadIdx.x - 1;  // GRAD coordinate of this thread (threads 1 .. d)
@@ -2682,8 +2648,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ mux_all,
                                                        const double* __restrict__ wts,
                                                        const int* __restrict__ dupv, long long cov_stride,
-                                                       int bpad, double* __restrict__ hout, int split,
-                                                       int* __restrict__ wq, unsigned* __restrict__ wqctl) {
+                                                       int bpad, double* __restrict__ hout, int split) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
   // 1-D grid: the `split` workgroups of one candidate side by side on one XCD (xcd_group), so its line
@@ -2691,184 +2656,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
   int b, g;
   if (!xcd_group(blockIdx.x, B, split, b, g)) return;
   envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
-                                       dupv, cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout,
-                                       wq, wqctl);
-}
-
-// ---------------------------------------------------------------------------
-// Split envelope, second kernel (staged forward, S <= 16, no kg_pairs): the pairs envelope_kernel's flat test
-// did not settle (its queue wq, count wqctl[0]), one wave per pair, each wave claiming the next queued pair
-// (wqctl[1]) until the queue is drained.  In one launch a workgroup waits for its slowest pair: with the walked
-// pairs (about 1 in 9 at the headline, each several times a flat pair's work) spread over the flat pairs'
-// workgroups, most workgroups lasted as long as one walked pair while their other waves idled.  Here the flat
-// workgroups end early and the walked pairs run side by side, one per wave.
-// Per pair the same code as envelope_body's: the lines (build_lines' arithmetic, the records read from global
-// memory instead of the staged copy), the same top hint and env_pair_regs with the flat test enabled (it
-// fails again: the pair was queued because it did), so KG_w has the bits the one-kernel envelope gives.  The
-// value goes to the group's row of wg_part (write-through); the group's last queued pair sums the group's
-// pair values in pair order and adds G_g / S onto kg[b], as envelope_body's combine does.
-constexpr int EW_WAVES = 4;
-// 2 waves per SIMD: the per-wave LDS (20 KiB at the headline) allows two 4-wave workgroups per CU anyway
-#ifndef EW_WAVES_PER_EU
-#define EW_WAVES_PER_EU 2
-#endif
-
-// LDS of one walk wave: the candidate's covariance records (front pad, NaN padding to every register slot) and
-// the survivor list (slopes, intercepts, line indices).
-__host__ __device__ inline size_t walk_wave_doubles(int N, int MP) {
-  return (size_t)stage_stride(N, MP) + 2 * ENV_CAP + ENV_CAP / 2;
-}
-
-template <int MAXL, int M>
-__global__ __launch_bounds__(EW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(EW_WAVES_PER_EU))) void envelope_walk_kernel(
-    const Plan* __restrict__ P, double* __restrict__ kg, const double* __restrict__ mu_all,
-    const double* __restrict__ cov_all, const double* __restrict__ var_all, const double* __restrict__ mux_all,
-    const double* __restrict__ wts, const int* __restrict__ dupv, long long cov_stride, int bpad,
-    const int* __restrict__ wq, unsigned* __restrict__ wqctl, unsigned cap) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int MP = cov_rec(M);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int m = P->m, N = P->N, NL = N + 1, S = P->S, target = P->target;
-  const bool full = target < 0;
-  const int ng = (S + 7) >> 3;
-  double* wbase = smem + (size_t)wave * walk_wave_doubles(N, MP);
-  double* lcv = wbase + STAGE_FRONT;               // record r at lcv + r * MP (record -1: the front pad)
-  double* sb = wbase + stage_stride(N, MP);
-  double* sa = sb + ENV_CAP;
-  int* si = reinterpret_cast<int*>(sa + ENV_CAP);
-  const int pad_end = (64 * MAXL - 1) * MP;       // records N .. 64 MAXL - 2: the padding lines
-  const unsigned count = min(wqctl[0], cap);      // written by the previous kernel (at most B S pairs)
-  for (;;) {
-    unsigned idx = 0;
-    if (lane == 0) idx = atomicAdd(&wqctl[1], 1u);
-    idx = __builtin_amdgcn_readfirstlane(idx);
-    if (idx >= count) break;
-    const int code = __builtin_amdgcn_readfirstlane(wq[idx]);
-    const int b = code / S, j = code % S;
-    const double* cvb = cov_all + (size_t)b * cov_stride;
-    // the candidate's records into this wave's LDS (envelope_body's staging, one wave), in flight while the
-    // coefficients are formed; the previous pair's reads of the region are done (its walk waited on them)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    dma_to_lds(cvb, lcv, N * MP, 0, 1, lane);
-    // the candidate's posterior at x_b and line 0's inputs (envelope_body's s_pp)
-    double sv[M], mx0[M], ysd[M], ymu[M], nz[M], l0m[M], l0v[M];
-    const int dupk = __builtin_amdgcn_readfirstlane(dupv[b]);
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const bool live = i < m;
-      ysd[i] = live ? P->o[i].y_std : 1.0;
-      ymu[i] = live ? P->o[i].y_mean : 0.0;
-      nz[i] = live ? P->o[i].noise : 0.0;
-      sv[i] = live ? var_all[(size_t)i * bpad + b] : 0.0;
-      mx0[i] = live ? mux_all[(size_t)i * bpad + b] : 0.0;
-      l0m[i] = mx0[i];
-      l0v[i] = sv[i];
-      if (dupk != DUP_NONE && live) {  // line 0 from record dupk, the same bits as line dupk + 1
-        l0m[i] = mu_all[(size_t)dupk * MP + i];
-        l0v[i] = cvb[(size_t)dupk * MP + i];
-      }
-    }
-    double w[M], wa[M], wb[M];
-    double a_off, den;
-    pair_coefs<M>(wts + (size_t)j * m, m, full, target, ysd, ymu, nz, sv, w, wa, wb, a_off, den);
-    double wbt = 0.0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) wbt = (i == target) ? wb[i] : wbt;
-    // wave-uniform: SGPRs, not VGPRs, while the lines are live (envelope_body likewise)
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      wa[i] = sgpr_f64(wa[i]);
-      wb[i] = sgpr_f64(wb[i]);
-      l0m[i] = sgpr_f64(l0m[i]);
-      l0v[i] = sgpr_f64(l0v[i]);
-    }
-    a_off = sgpr_f64(a_off);
-    wbt = sgpr_f64(wbt);
-    // envelope_body's top hint (Plan::itop): the same inputs, the same decision (line k1's slope below, once
-    // the records have landed)
-    double a0 = a_off, b0 = 0.0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      a0 = fma(wa[i], l0m[i], a0);
-      b0 = fma(wb[i], l0v[i], b0);
-    }
-    const double A1 = P->itop[j];
-    const int k1 = P->itopk[2 * j], c1 = P->itopk[2 * j + 1];
-    // this scalarisation's intercepts a_k from the plan's cache (Plan::icpt: build_lines' intercepts, bit for
-    // bit); NaN at slot 0 (line 0 is built here) and past N
-    const gdptr icp = uniform_gptr(P->icpt + (size_t)j * P->icpt_stride);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int e = N * MP + lane; e < pad_end; e += 64) lcv[e] = __builtin_nan("");  // (incl. the DMA's tail)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    auto rec_dot = [&](const double* r, const double (&c)[M], double acc) __attribute__((always_inline)) {
-      if constexpr (MP == 1) {
-        acc = fma(c[0], r[0], acc);
-      } else {
-#pragma unroll
-        for (int q = 0; 2 * q < M; ++q) {
-          const double2 u = *reinterpret_cast<const double2*>(r + 2 * q);
-          acc = fma(c[2 * q], u.x, acc);
-          if (2 * q + 1 < M) acc = fma(c[2 * q + 1], u.y, acc);
-        }
-      }
-      return acc;
-    };
-    TopHint hint{false, 0.0, 0.0};
-    if (DKG_TOP_HINT) {
-      if (a0 > A1) {
-        hint = TopHint{true, a0, b0};
-      } else if (a0 < A1 && c1 == 1) {
-        const double* r = lcv + (size_t)(k1 - 1) * MP;
-        hint = TopHint{true, A1, full ? rec_dot(r, wb, 0.0) : wbt * r[target]};
-      }
-    }
-    // build_lines' lines: a_k from the cache, b_k from the staged records; line 0 the candidate
-    auto build = [&](double (&la)[MAXL], double (&lb)[MAXL]) {
-      const double* cvr = lcv + (lane - 1) * MP;
-#pragma unroll
-      for (int t = 0; t < MAXL; ++t) {
-        la[t] = icp[lane + 64 * t];
-        lb[t] = full ? rec_dot(cvr + 64 * MP * t, wb, 0.0) : wbt * cvr[64 * MP * t + target];
-      }
-      double a = a_off, bb = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        a = fma(wa[i], l0m[i], a);
-        bb = fma(wb[i], l0v[i], bb);
-      }
-      la[0] = (lane == 0) ? a : la[0];
-      lb[0] = (lane == 0) ? bb : lb[0];
-    };
-    int hn = 1;
-    const double kgj = env_pair_regs<MAXL>(build, NL, lane, sb, sa, si, false, &hn, nullptr, nullptr, true,
-                                           static_cast<const int*>(nullptr), hint);
-    // the group's row: this pair's value, then the group's count; its last queued pair sums the group
-    const size_t prow = (size_t)b * (S + ng);
-    int* tk = P->tickets + (size_t)b * (ng + 1);
-    const int grp = j >> 3;
-    // The lane-0 sections end in wave-uniform values (readfirstlane) and the body ends in a wave barrier:
-    // without them the compiler let lanes 1..63 skip a lane-0 tail straight back to the claim as a loop of
-    // their own, where the claim's readfirstlane read a lane that never claimed (pair 0 again, forever).
-    int last = 0;
-    if (lane == 0) {
-      __hip_atomic_store(&P->wg_part[prow + j], kgj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      last = __hip_atomic_fetch_add(&tk[grp], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
-    }
-    last = __builtin_amdgcn_readfirstlane(last);
-    if (last) {  // wave-uniform: every lane sums the group's values (the same loads, the same order)
-      const int gpairs = min(8, S - 8 * grp);
-      double gsum = 0.0;
-      for (int q = 8 * grp; q < 8 * grp + gpairs; ++q)
-        gsum += __hip_atomic_load(&P->wg_part[prow + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0) atomicAdd(&kg[b], gsum / (double)S);
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
+                                       dupv, cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout);
 }
 
 // The lines of every (candidate, scalarisation) pair of the plan's last
@@ -2939,30 +2727,15 @@ struct EnvLaunch {
   const double* xnew;  // GRAD
   double* dkg;         // GRAD
   double* hout;        // GRAD: pinned host [kg | dkg] (dkg_plan_forward_grad_hostx), nullable
-  bool split = false;  // the split envelope (envelope_walk_kernel after envelope_kernel): staged forward only
 };
 
 template <int MAXL, int M, bool GRAD, bool STREAM>
 hipError_t launch_env_t(const EnvLaunch& a) {
   raise_lds_limit((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>, a.lds);
   const Plan& h = *a.host;
-  const bool split = !GRAD && !STREAM && a.split;
   hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights, h.dup,
-                     (long long)h.cov_stride, h.bpad, a.hout, h.split, split ? h.wq : nullptr,
-                     split ? h.wqctl : nullptr);
-  if constexpr (!GRAD && !STREAM) {
-    if (split) {
-      // persistent: at most 4 workgroups (16 waves) per CU, fewer when the batch has fewer pairs
-      const long long waves = (long long)a.B * h.S;
-      const int grid = (int)std::max(1LL, std::min(1024LL, (waves + EW_WAVES - 1) / EW_WAVES));
-      const size_t wlds = (size_t)EW_WAVES * walk_wave_doubles(h.N, cov_rec(M)) * sizeof(double);
-      raise_lds_limit((const void*)envelope_walk_kernel<MAXL, M>, wlds);
-      hipLaunchKernelGGL((envelope_walk_kernel<MAXL, M>), dim3(grid), dim3(EW_WAVES * WAVE), wlds, a.s, a.dev, a.kg,
-                         h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights, h.dup, (long long)h.cov_stride, h.bpad,
-                         h.wq, h.wqctl, (unsigned)waves);
-    }
-  }
+                     (long long)h.cov_stride, h.bpad, a.hout, h.split);
   return hipGetLastError();
 }
 

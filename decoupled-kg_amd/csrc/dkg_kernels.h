@@ -102,10 +102,6 @@ struct Plan {
   int32_t icpt_stride;              // 64 * env_slots(N + 1): one entry per register slot of the envelope
   double* itop;                     // [S]: max_{k >= 1} a_k (-inf when N = 0)
   int* itopk;                       // [S][2]: the first k >= 1 attaining it, and how many lines do
-  // Split envelope (staged forward): the pairs the flat test leaves, queued (b S + j) by envelope_kernel for
-  // envelope_walk_kernel; wqctl [0] queued, [1] claimed (zeroed by the cross stage)
-  int* wq;                          // [max_B x S]
-  unsigned* wqctl;                  // [2]
 };
 
 // By-value arguments of the state-preparation use of the cross stage.

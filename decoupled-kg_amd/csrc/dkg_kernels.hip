@@ -191,7 +191,6 @@ __device__ inline void clear_tile_accumulators(const Plan* __restrict__ P, doubl
     P->dup[i] = DUP_NONE;
   }
   for (int i = b0 * ng1 + (int)threadIdx.x; i < b1 * ng1; i += blockDim.x) P->tickets[i] = 0;
-  if (ti == 0 && threadIdx.x < 2) P->wqctl[threadIdx.x] = 0u;  // the split envelope's queue
 }
 
 // Forward: grid (B tiles, pairs, outputs); the first workgroup of every row tile also clears that
@@ -546,17 +545,6 @@ void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow)
   *split = (S + sw - 1) / sw;
 }
 
-// The split envelope (envelope_walk_kernel for the pairs the flat test leaves) for the staged forward: at most
-// two groups of 8 pairs per candidate (the groups meet by commutative adds), no per-pair outputs, no test hooks.
-// Off unless DKG_ENV_SPLIT=1: measured slower than the one-kernel envelope at every shape tried (DESIGN.md 4.9:
-// headline G = 1 11.0 -> 35.6 us, G = 20 103.6 -> 131.6 us, headline_nd G = 20 124.5 -> 964 us).
-static bool env_split(const Plan& h, const double* pairs) {
-  static const char* env = std::getenv("DKG_ENV_SPLIT");
-  if (!env || std::atoi(env) != 1) return false;
-  return h.stream == 0 && !h.f32 && pairs == nullptr && h.S <= 16 && h.debug_env == 0 && h.debug_stamp == 0 &&
-         !DKG_ICP;
-}
-
 // The envelope launch for the plan's output bucket.
 template <bool GRAD>
 static hipError_t launch_env(const Plan& h, const EnvLaunch& a) {
@@ -584,7 +572,6 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
   EnvLaunch a{&h, dev, B, kg, pairs, dim3(xcd_group_size(B, h.split)), dim3(h.sw * WAVE),
               envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0, false, !DKG_ICP), s, h.debug_stamp, nullptr,
               nullptr};
-  a.split = env_split(h, pairs);
   return launch_env<false>(h, a);
 }
 
