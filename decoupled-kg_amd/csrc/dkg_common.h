@@ -495,6 +495,48 @@ __device__ __forceinline__ bool xcd_group(int L, int nblk, int groups, int& blk,
   return blk < nblk;
 }
 
+// Block order of a launch over (column block bx < nbx, row block by < nby, output oi < m) whose workgroups
+// each read a row panel (by, oi) and a column panel (bx, oi): order 0 is xcd_group's (the outputs of one block
+// side by side, blocks dealt over the XCDs); orders 1 and 2 give every XCD a contiguous range of the task list
+// [bx][by][oi] (1) or [oi][bx][by] (2), so the workgroups resident on one XCD at once share panels in its L2
+// (the ids L and L + 8 share an XCD: XCD L % 8 takes tasks (L % 8) tpx + L / 8, tpx = ceil(tasks / 8)).
+// Order 3: XCD x owns the column blocks [x cb, x cb + cb), cb = ceil(nbx / 8), in the order [oi][bx][by].
+__host__ __device__ inline int block_order_size(int nbx, int nby, int m, int order) {
+  if (order == 3) return 8 * ((nbx + 7) / 8) * nby * m;
+  return order == 0 ? xcd_group_size(nbx * nby, m) : 8 * ((nbx * nby * m + 7) / 8);
+}
+__device__ __forceinline__ bool block_order(int L, int nbx, int nby, int m, int order, int& bx, int& by, int& oi) {
+  if (order == 0) {
+    int blk;
+    if (!xcd_group(L, nbx * nby, m, blk, oi)) return false;
+    bx = blk % nbx;
+    by = blk / nbx;
+    return true;
+  }
+  if (order == 3) {
+    const int cb = (nbx + 7) / 8, r = L >> 3;
+    by = r % nby;
+    bx = (L & 7) * cb + (r / nby) % cb;
+    oi = r / (nby * cb);
+    return bx < nbx;
+  }
+  const int T = nbx * nby * m, tpx = (T + 7) / 8;
+  const int t = (L & 7) * tpx + (L >> 3);
+  if (t >= T) return false;
+  if (order == 1) {
+    oi = t % m;
+    const int u = t / m;
+    by = u % nby;
+    bx = u / nby;
+  } else {
+    by = t % nby;
+    const int u = t / nby;
+    bx = u % nbx;
+    oi = u / nbx;
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // In-launch hand-offs (the fused one-launch forward, dkg_fused.h), MI355X_MICROARCH.md
 // "inter-workgroup visibility" / cdna_hip_programming.md Guideline 16, counter form:

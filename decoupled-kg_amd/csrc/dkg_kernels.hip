@@ -478,6 +478,19 @@ static bool cov_big(int N, int B, int m) {
   return N >= 128 && (size_t)((N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)) * m >= 256;
 }
 
+// The big blocks' order (block_order).  Measured per launch (L2 fetch x2 / write MB, stage us; DESIGN.md 4.7,
+// profiles/r05/cov_order): stress (nbx 64, nby 4, m 3): order 0 363 / 37, 1 263 / 36, 2 145 / 101, 3 152 / 101,
+// all 143 us; headline x 10 (nbx 16, nby 20, m 2): 0 49 / 21, 1 72 / 21, 2 44 / 42, all 47 us.  Orders 2 / 3
+// read each panel about once but write every output's record sectors separately (3x the records); order 1 keeps
+// the outputs of a block side by side (whole records leave L2) and shares the line panels of a wide launch.
+// DKG_COV_ORDER=0..3 (A/B measurements) forces it.
+static int cov_big_order(int nbx, int nby, int m) {
+  static const char* env = std::getenv("DKG_COV_ORDER");
+  if (env) return std::atoi(env);
+  (void)m;
+  return nbx >= 4 * nby ? 1 : 0;
+}
+
 template <int DM, class T>
 static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const double* xnew, int B, double* kg,
                                       hipStream_t s, int stage, int geom_B) {
@@ -496,10 +509,12 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
   }
   if constexpr (sizeof(T) == 8 && DM <= 8) {  // (d > 8: the big blocks' kernel terms spill)
     if (cov_big(h.N, B, h.m)) {
-      dim3 grid(xcd_group_size(((h.N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)), h.m));
+      const int nbx = (h.N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
+      const int order = cov_big_order(nbx, nby, h.m);
+      dim3 grid(block_order_size(nbx, nby, h.m, order));
       raise_lds_limit((const void*)posterior_cov_big_kernel<DM>, PB_LDS);
       hipLaunchKernelGGL((posterior_cov_big_kernel<DM>), grid, dim3(PB_WAVES * WAVE), PB_LDS, s, dev, xnew, B,
-                         h.debug_stamp);
+                         h.debug_stamp, order);
       return hipGetLastError();
     }
   }

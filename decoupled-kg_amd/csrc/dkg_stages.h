@@ -719,16 +719,15 @@ constexpr size_t PB_LDS = PB_NSTG * (size_t)PB_STAGE * 16 + (size_t)PB_WAVES * 1
 
 template <int DM>
 __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_big_kernel(
-    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst) {
+    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst, int order) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double2* stg = reinterpret_cast<double2*>(smem);
   const int N = P->N;
   const int nbx = (N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
-  int blk, oi;
-  if (!xcd_group(blockIdx.x, nbx * nby, P->m, blk, oi)) return;
+  int bx, by, oi;
+  if (!block_order(blockIdx.x, nbx, nby, P->m, order, bx, by, oi)) return;
   unsigned long long* st = kst_slot(dst, P, 1);
   KST_BEGIN(st);
-  const int bx = blk % nbx, by = blk / nbx;
   const dkg_output& o = P->o[oi];
   const int d = P->d;
   const int lane = threadIdx.x & 63;

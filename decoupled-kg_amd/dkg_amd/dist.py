@@ -141,6 +141,9 @@ class ShardedDiscreteKG:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # the exchange runs whenever a process group exists (world size 1 included: one RCCL / gloo
+        # collective over a single rank), and is skipped without one
+        self.collective = dist.is_initialized()
         self.W = scalarisation_weights
         self.S = scalarisation_weights.shape[0]
         self.d = x_discretisation.shape[-1]
@@ -173,7 +176,7 @@ class ShardedDiscreteKG:
         flat = X.reshape(-1, self.d)
         B = flat.shape[0]
         cdev = self._comm_device(flat)
-        if self.world > 1 and flat.requires_grad:
+        if self.collective and flat.requires_grad:
             flat = _SumGradOverRanks.apply(flat, cdev, self.group)
         if self.axis == "scalarisations":
             n_local = self.w_hi - self.w_lo
@@ -181,7 +184,7 @@ class ShardedDiscreteKG:
                 part = self._local(flat, self.W[self.w_lo:self.w_hi]).to(cdev, torch.double) * n_local
             else:
                 part = _zeros_like_graph(flat, B, cdev)
-            if self.world > 1:
+            if self.collective:
                 part = _AllReduceSum.apply(part, self.group)
             out = part / self.S
         else:
@@ -194,7 +197,7 @@ class ShardedDiscreteKG:
             if pad > 0 or not pieces:
                 pieces.append(_zeros_like_graph(flat, pad, cdev))
             mine = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
-            allv = _AllGather.apply(mine, self.world, self.rank, self.group) if self.world > 1 else mine
+            allv = _AllGather.apply(mine, self.world, self.rank, self.group) if self.collective else mine
             out = allv[:B]
         return out.to(X.device).reshape(batch_shape)
 
@@ -220,14 +223,14 @@ class ShardedDiscreteKG:
                 buf = torch.zeros(B, dtype=torch.double, device=cdev)
             buf = buf.contiguous()
             work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True) \
-                if self.world > 1 else _Done()
+                if self.collective else _Done()
             return PendingKG(work, lambda: (buf / self.S).to(X.device).reshape(batch_shape))
         chunk = -(-B // self.world) if B > 0 else 0
         lo, hi = shard_range(B, self.rank, self.world)
         mine = torch.zeros(chunk, dtype=torch.double, device=cdev)
         if hi > lo:
             mine[:hi - lo] = self._local(flat[lo:hi], self.W).detach().to(cdev, torch.double)
-        if self.world == 1:
+        if not self.collective:
             return PendingKG(_Done(), lambda: mine[:B].to(X.device).reshape(batch_shape))
         allv = torch.empty(chunk * self.world, dtype=torch.double, device=cdev)
         if cdev.type == "cuda":
@@ -268,6 +271,7 @@ class BatchExchange:
         if mode not in ("gather", "reduce"):
             raise ValueError(f"mode must be 'gather' or 'reduce', got {mode!r}")
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.collective = dist.is_initialized()  # as ShardedDiscreteKG: world size 1 included
         self.B, self.E, self.mode, self.S_local = int(B), max(1, int(every)), mode, S_local
         self.bufs = [torch.zeros(self.E, self.B, dtype=dtype, device=device) for _ in range(2)]
         self.gathered = [torch.zeros(self.world * self.E * self.B, dtype=dtype, device=device) for _ in range(2)]
@@ -308,7 +312,7 @@ class BatchExchange:
 
     def _exchange(self, slot: int, rows: int) -> None:
         self.rows[slot] = rows
-        if self.world == 1:
+        if not self.collective:
             if self.mode == "gather":
                 self.gathered[slot][:rows * self.B].copy_(self.bufs[slot][:rows].reshape(-1))
             self.works[slot] = _Done()

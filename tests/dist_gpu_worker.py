@@ -1,8 +1,10 @@
-"""Rank body for tests/test_gpu_dist.py: the HIP forward sharded over 2 ranks on one GPU.
+"""Rank body for tests/test_gpu_dist.py and tests/test_gpu_rccl.py: the HIP forward sharded over ranks.
 
-torch.distributed with gloo (both ranks on cuda:0; RCCL needs one GPU per rank).  Rank r
-evaluates its shard through DiscreteKnowledgeGradient (the C ABI); rank 0 also runs the
-unsharded forward and writes everything for the test process.
+usage: dist_gpu_worker.py WORKLOAD OUT [BACKEND]
+torch.distributed with gloo (test_gpu_dist: 2 ranks, both on cuda:0) or nccl = RCCL (test_gpu_rccl:
+1 rank on cuda:0; RCCL needs one GPU per rank).  Rank r evaluates its shard through
+DiscreteKnowledgeGradient (the C ABI); rank 0 also runs the unsharded forward and writes everything
+for the test process.
 """
 
 import os
@@ -24,10 +26,14 @@ from dkg_amd.synthetic import WORKLOADS, make_problem  # noqa: E402
 
 def main():
     workload, out = sys.argv[1], sys.argv[2]
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
+    backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+    rank, world = dist.get_rank(), dist.get_world_size()
     model, D, X, W = make_problem(WORKLOADS[workload])
     res = {}
     for target in (None, 1):
@@ -38,6 +44,7 @@ def main():
             wts = torch.linspace(0.5, 1.5, X.shape[0], dtype=torch.double)
             (acq(Xr.unsqueeze(-2)) * wts).sum().backward()
             res[(axis, target)] = (kg.cpu(), Xr.grad.clone())
+            res[("async", axis, target)] = acq.forward_async(X.unsqueeze(-2)).wait().cpu()
     # bench.py's exchange: K forward batches per collective, both modes, HIP forwards into the rows
     B, S = X.shape[0], W.shape[0]
     for mode in ("reduce", "gather"):
@@ -70,6 +77,10 @@ def main():
             (kg * wts).sum().backward()
             ref[target] = (kg.detach().cpu(), Xr.grad.cpu())
         torch.save({"ranks": allres, "ref": ref}, out)
+    res_backend = dist.get_backend()
+    if rank == 0:
+        with open(out + ".backend", "w") as f:
+            f.write(f"{res_backend} world={world}")
     dist.destroy_process_group()
 
 

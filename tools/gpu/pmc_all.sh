@@ -1,12 +1,16 @@
 #!/bin/bash
 # PMC passes (tools/pmc_passes.sh) for each benched workload at the launch shape of the driver's run
 # (--steps 20, two streams: 10 forward batches per launch), aggregated into <out>/pmc_<workload>.json (copied
-# into profiles/r05/).  The stress leg runs one forward per launch (bench.py), so its passes use 1.
+# into profiles/r05/).  The stress legs run one forward per launch (bench.py), so their passes use 1.
+# usage: tools/gpu/pmc_all.sh <out> [workload[:fp32] ...]   (default: headline headline_nd stress)
 set -uo pipefail
-out=${1:-gpurun_out/pmc}
-for wl in headline headline_nd stress; do
-  g=10; [ "$wl" = stress ] && g=1
-  bash tools/pmc_passes.sh "$out/$wl" --workload "$wl" --batches-per-launch $g || exit 1
-  python3 tools/pmc_report.py "$out/$wl" "$out/${wl}_report.json" "$out/pmc_${wl}.json" > "$out/${wl}_report.txt" || exit 1
+out=${1:-gpurun_out/pmc}; shift || true
+wls=${*:-headline headline_nd stress}
+for spec in $wls; do
+  wl=${spec%%:*}; prec=fp64; tag=$wl
+  [ "$spec" != "$wl" ] && { prec=${spec#*:}; tag=${wl}_$prec; }
+  g=10; case $wl in stress*) g=1;; esac
+  bash tools/pmc_passes.sh "$out/$tag" --workload "$wl" --precision "$prec" --batches-per-launch $g || exit 1
+  python3 tools/pmc_report.py "$out/$tag" "$out/${tag}_report.json" "$out/pmc_${tag}.json" > "$out/${tag}_report.txt" || exit 1
 done
 ls -la "$out"

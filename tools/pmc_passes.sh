@@ -7,7 +7,7 @@ set -uo pipefail
 out=$1; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
-B="python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 --profile-reps 2 --grad-steps 0 --b1-calls 0 --nd-steps 0 --stress-steps 0 --streams 1 --graph 0 $*"
+B="python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 --profile-reps 2 --grad-steps 0 --b1-calls 0 --nd-steps 0 --stress-steps 0 --stress32-steps 0 --streams 1 --graph 0 $*"
 timeout -s KILL 60 rocprofv3 -L > "$out/counters_list.txt" 2>&1 || true
 pass() {
   local name=$1; shift
