@@ -18,7 +18,8 @@ __host__ __device__ constexpr int pair_groups(int S) { return (S + 7) >> 3; }
 constexpr int DUP_NONE = 0x7fffffff;
 
 // Stage ablations (empty cross / covariance / envelope launches selected by
-// DKG_DEBUG_COV_FLAGS 2 / 1 and DKG_DEBUG_ENV_FLAGS 2) exist only in builds
+// DKG_DEBUG_COV_FLAGS 2 / 1 and DKG_DEBUG_ENV_FLAGS 2; cross_big_kernel's means alone / Q_X blocks alone by
+// DKG_DEBUG_COV_FLAGS 16 / 32) exist only in builds
 // with -DDKG_ABLATIONS=1: the check is a dependent scalar load at kernel entry.
 #ifndef DKG_ABLATIONS
 #define DKG_ABLATIONS 0

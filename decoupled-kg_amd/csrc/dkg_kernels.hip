@@ -224,6 +224,70 @@ __global__ __launch_bounds__(KF_WAVES * WAVE) void cross_kfill_kernel(const Plan
   cross_kfill_body<DM>(P->o[oi], P->d, xnew, B, P->kx[oi], blockIdx.x, blockIdx.y * KF_KB);
 }
 
+// The cross stage of a launch with the K(x, X) fill (cross_kfill_launch) in one launch: the 64 x 32 blocks of
+// Q_X (cross_big_body, the longest first), then RT x m workgroups for the means K(x, X) alpha + c and the
+// accumulator clears.  The means follow cross_root_impl's arithmetic element for element -- its fill loop's
+// per-thread fma order over the 512 threads of a row tile (thread t here runs the chains of threads t and
+// t + 256), the lane-group adds, the 8 waves in order -- so they have the bits of the one-kernel cross stage.
+__global__ __launch_bounds__(XB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void cross_big_kernel(
+    const Plan* __restrict__ P, int B, double* __restrict__ kg) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nbig = cross_big_blocks(P->max_np, B, P->m);
+  if ((int)blockIdx.x < nbig) {
+    if (DKG_ABLATIONS && (P->debug_cov & 16)) return;  // probe: the means alone
+    cross_big_body(P, B, blockIdx.x, smem);
+    return;
+  }
+  if (DKG_ABLATIONS && (P->debug_cov & 32)) return;  // probe: the Q_X blocks alone
+  const int RT = pad16(B) / 16;
+  const int ti = (blockIdx.x - nbig) % RT, oi = (blockIdx.x - nbig) / RT;
+  if (oi == 0) clear_tile_accumulators(P, kg, B, ti);
+  const dkg_output& o = P->o[oi];
+  const int n = o.n, KB = pad16(n) / 4;
+  const double* kx = P->kx[oi];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool rv = ti * 16 + (lane & 15) < B;
+  constexpr int VT = CR_WAVES * WAVE;  // the threads of cross_root_impl's fill
+  constexpr int CH = VT / (XB_WAVES * WAVE);
+  static_assert(CH == 2, "two fill chains per thread");
+  const int iters = (KB * 64 + VT - 1) / VT;
+  double mpart[CH] = {0.0, 0.0};
+  constexpr int U = 8;  // loads issued ahead of their fmas
+  for (int it0 = 0; it0 < iters; it0 += U) {
+    double kv[CH][U], al[CH][U];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + c * XB_WAVES * WAVE + min(it0 + u, iters - 1) * VT;
+        const int col = 4 * (e >> 6) + (lane >> 4);
+        kv[c][u] = (rv && col < n) ? kx[frag_index(ti, min(e >> 6, KB - 1), lane, KB)] : 0.0;
+        al[c][u] = o.alpha[min(col, n - 1)];
+      }
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (it0 + u < iters) mpart[c] = fma(kv[c][u], al[c][u], mpart[c]);
+  }
+  __shared__ double mred[CR_WAVES * 16];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    double v = mpart[c];
+    v += partner_f64<4>(v);
+    v += partner_f64<5>(v);
+    if (lane < 16) mred[(wave + c * XB_WAVES) * 16 + lane] = v;
+  }
+  __syncthreads();
+  if (tid < 16) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < CR_WAVES; ++w) s += mred[w * 16 + tid];
+    const int rr = ti * 16 + tid;
+    P->mux[oi][rr] = (rr < B) ? o.mean_constant + s : 0.0;
+  }
+}
+
 // Value + gradient cross stage, one launch: grid (B tiles, pairs, m + m d).
 // z < m: the forward cross stage of output z (Q_X fragment-packed and row-major, means; kg and the
 // tickets cleared).  z >= m, z - m = oi d + g: J_g = dK(x, X)/dx_g R (row-major) and dmean/dx_g for
@@ -478,6 +542,13 @@ static bool cov_big(int N, int B, int m) {
   return N >= 128 && (size_t)((N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)) * m >= 256;
 }
 
+// The cross stage of a launch with the K(x, X) fill as 64 x 64 blocks (cross_big_kernel); DKG_CROSS_BIG=0 (A/B
+// measurements) keeps cross_root_plan_kernel.
+static bool cross_big() {
+  static const char* env = std::getenv("DKG_CROSS_BIG");
+  return !env || std::atoi(env) != 0;
+}
+
 // The big blocks' order (block_order).  Measured per launch (L2 fetch x2 / write MB, stage us; DESIGN.md 4.7,
 // profiles/r05/cov_order): stress (nbx 64, nby 4, m 3): order 0 363 / 37, 1 263 / 36, 2 145 / 101, 3 152 / 101,
 // all 143 us; headline x 10 (nbx 16, nby 20, m 2): 0 49 / 21, 1 72 / 21, 2 44 / 42, all 47 us.  Orders 2 / 3
@@ -499,6 +570,14 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
     if (use_kx) {
       dim3 kgrid(pad16(B) / 16, (h.max_np / 4 + KF_KB - 1) / KF_KB, h.m);
       hipLaunchKernelGGL((cross_kfill_kernel<DM>), kgrid, dim3(KF_WAVES * WAVE), 0, s, dev, xnew, B);
+    }
+    if constexpr (sizeof(T) == 8) {
+      if (use_kx && cross_big()) {  // K(x, X) in place: the 64 x 64 blocks, then the means and the clears
+        raise_lds_limit((const void*)cross_big_kernel, XB_LDS);
+        hipLaunchKernelGGL(cross_big_kernel, dim3(cross_big_blocks(h.max_np, B, h.m) + pad16(B) / 16 * h.m),
+                           dim3(XB_WAVES * WAVE), XB_LDS, s, dev, B, kg);
+        return hipGetLastError();
+      }
     }
     dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);

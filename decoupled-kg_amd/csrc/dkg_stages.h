@@ -99,8 +99,9 @@ __device__ __forceinline__ double cross_kernel_term(const double (&xr)[DM], cons
   return os * kernel_profile_t<KIND>(r2, tab);
 }
 
-// K(x_b, X_j) of output o for a row tile ti and KF_KB k-blocks, in the cross stage's B-operand order
-// (element e = kb * 64 + l: row 16 ti + (l & 15), column 4 kb + (l >> 4)); zero outside B x n.
+// K(x_b, X_j) of output o for a row tile ti and KF_KB k-blocks, in the cross stage's B-operand order, pair-packed
+// (frag_index: row 16 ti + (l & 15), column 4 kb + (l >> 4); the k-blocks 2 j, 2 j + 1 of a lane in one 16-byte
+// word, as R^T's fragments, so cross_big_kernel stages both operands alike); zero outside B x n.
 template <int DM>
 __device__ __forceinline__ void cross_kfill_body(const dkg_output& o, int d, const double* __restrict__ x, int rows,
                                                  double* __restrict__ kx, int ti, int kb0) {
@@ -127,7 +128,7 @@ __device__ __forceinline__ void cross_kfill_body(const dkg_output& o, int d, con
 #pragma unroll
       for (int k = 0; k < DM; ++k) xs[k] = o.train_x[(size_t)cc * d + min(k, d - 1)] * o.inv_lengthscale[min(k, d - 1)];
       const double kv = cross_kernel_term<DM, KIND>(xr, xs, d, os, tab);
-      kx[((size_t)ti * KB + kb) * 64 + lane] = (rv && col < n) ? kv : 0.0;
+      kx[frag_index(ti, kb, lane, KB)] = (rv && col < n) ? kv : 0.0;
     }
   };
   switch (o.kernel) {
@@ -254,7 +255,7 @@ __device__ __forceinline__ void cross_root_impl(const dkg_output& o, int d, cons
         }
         kv = os * kernel_dprofile_t<KIND>(r2) * (xg - xs[(size_t)cc * d + gdim]) * ilg;
       } else if constexpr (KIND < 0) {
-        kv = kx[(size_t)ti * KB * 64 + min(e, KB * 64 - 1)];  // zero outside B x n
+        kv = kx[frag_index(ti, min(e >> 6, KB - 1), lane, KB)];  // zero outside B x n (e & 63 == lane)
       } else {
         kv = cross_kernel_term<DM, KIND>(xr, xs + (size_t)cc * d, d, os, tab);
       }
@@ -960,6 +961,172 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
     }
   }
   KST_END(st);
+}
+
+// ---------------------------------------------------------------------------
+// cross_big_kernel (fp64 forward, launches with the K(x, X) fill, cross_kfill_launch): Q_X = K(x, X) R for
+// 64 x 32 blocks (4 candidate tiles x 2 column tiles of Q, one output) with cross_root_impl's arithmetic
+// element for element, so the two give the same bits and the choice is a speed matter only.  cross_root_impl
+// sums column tile tj of Q over the k range of its pair (tj, T - 1 - tj) split in 8 wave chunks of
+// cw = ceil(kbW / 16) words (kbW = 4 (max(tj, T - 1 - tj) + 1) k-blocks), each chunk as two k-block-parity
+// chains of MFMAs (R^T as the A operand, K as the B operand) added, the chunks summed in order from 0; the
+// tile's k range ends at 4 (tj + 1) (R upper triangular).  Here wave w keeps those chains and running sums for
+// column tile w % 2 against candidate tiles 2 (w / 2) and 2 (w / 2) + 1, flushing the chains at the tile's chunk
+// ends.  Operands staged through LDS by LDS-DMA as in posterior_cov_big_kernel: K is read once per 32 columns
+// instead of once per column pair, R once per 64 candidates instead of 16 (the stress cross stage's L2
+// fetches).  Blocks of 32 columns: the longest (k = n) takes 128 words x 4 MFMAs per wave at n = 1024, so the
+// triangle's longest blocks are not the whole stage; they are dispatched first, and the candidate blocks of one
+// column block and output sit side by side on one XCD (xcd_group), sharing its R panel.
+constexpr int XB_WAVES = 4;
+constexpr int XB_TT = 2;  // column tiles of Q (row tiles of R^T) per block
+constexpr int XB_RT = 4;  // candidate tiles per block
+constexpr int XB_WC = 4;  // words per staged chunk (one barrier per 16 MFMAs per wave)
+constexpr int XB_STAGE = (XB_TT + XB_RT) * XB_WC * 64;  // 16-byte words per stage buffer
+#ifndef DKG_XB_NSTG
+#define DKG_XB_NSTG 3
+#endif
+constexpr int XB_NSTG = DKG_XB_NSTG;  // stage buffers: chunks in flight during the current one's MFMAs
+constexpr size_t XB_LDS = XB_NSTG * (size_t)XB_STAGE * 16;
+
+__host__ __device__ inline int cross_big_blocks(int max_np, int B, int m) {
+  const int nbj = (max_np / 16 + XB_TT - 1) / XB_TT, nbi = (pad16(B) / 16 + XB_RT - 1) / XB_RT;
+  return xcd_group_size(nbj * m, nbi);
+}
+
+// One block of cross_big_kernel (dkg_kernels.hip: the launch also holds the means' workgroups), L its index.
+__device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B, int L, double* smem) {
+  double2* stg = reinterpret_cast<double2*>(smem);
+  const int m = P->m;
+  const int RT = pad16(B) / 16, nbi = (RT + XB_RT - 1) / XB_RT;
+  const int nbj = (P->max_np / 16 + XB_TT - 1) / XB_TT;
+  int blk, bi;
+  if (!xcd_group(L, nbj * m, nbi, blk, bi)) return;
+  const int bj = nbj - 1 - blk / m, oi = blk % m;
+  const dkg_output& o = P->o[oi];
+  const int np = pad16(o.n), T = np / 16, KB = np / 4, KP = KB / 2;
+  const int tj0 = XB_TT * bj, ti0 = XB_RT * bi;
+  if (tj0 >= T) return;  // an output with fewer training points than the widest
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rp = wave & 1, cp = wave >> 1;  // column tile tj0 + rp; candidate tiles ti0 + 2 cp, ti0 + 2 cp + 1
+  const double* rt = o.root_frag;
+  const double* kx = P->kx[oi];
+  const int W = 2 * min(tj0 + XB_TT, T);  // words the block reads: its last live column tile's k range
+  const int nc = (W + XB_WC - 1) / XB_WC;
+  constexpr int XB_PIECES = (XB_TT + XB_RT) * XB_WC / XB_WAVES;
+  static_assert((XB_TT + XB_RT) * XB_WC % XB_WAVES == 0 && XB_PIECES == 6, "six DMA pieces per wave per chunk");
+  auto stage = [&](int c) {
+    const int j0 = c * XB_WC, nw = min(XB_WC, W - j0);
+    double2* buf = stg + (size_t)(c % XB_NSTG) * XB_STAGE;
+#pragma unroll
+    for (int q = 0; q < XB_PIECES; ++q) {
+      const int piece = wave + XB_WAVES * q;
+      const int t = piece / XB_WC, w = min(piece % XB_WC, nw - 1);
+      const double* src = t < XB_TT ? rt : kx;
+      const int tile = t < XB_TT ? min(tj0 + t, T - 1) : min(ti0 + t - XB_TT, RT - 1);
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const void*>(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 2),
+          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(buf + piece * 64)),
+          16, 0, 0);
+    }
+  };
+  // the wave's column tile: live, k extent in words, chunk width in words (cross_root_impl's pair split)
+  const int tj = tj0 + rp;
+  const bool live = tj < T;
+  const int E = 2 * (tj + 1);
+  const int CW = (2 * (max(tj, T - 1 - tj) + 1) + CR_WAVES - 1) / CR_WAVES;  // kbW / 2 words over 8 chunks
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
+  const uint32_t addrA = lds0 + (uint32_t)((rp * XB_WC) * 64 + lane) * 16;
+  const uint32_t addrB = lds0 + (uint32_t)(((XB_TT + 2 * cp) * XB_WC) * 64 + lane) * 16;
+  d4 ch[2][2], sum[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    sum[h] = d4{0.0, 0.0, 0.0, 0.0};
+    ch[h][0] = ch[h][1] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  int seg_left = CW;  // words left in the current chunk of cross_root_impl's split
+#pragma unroll
+  for (int c = 0; c < XB_NSTG - 1; ++c)
+    if (c < nc) stage(c);
+  for (int c = 0; c < nc; ++c) {
+    // chunk c landed: the chunks issued after it (at most XB_NSTG - 2, six pieces each) may stay in flight
+    static_assert(XB_NSTG >= 2 && XB_NSTG <= 6, "vmcnt cases");
+    switch (min(nc - 1 - c, XB_NSTG - 2)) {  // wave-uniform
+      case 4: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+    asm volatile("s_barrier" ::: "memory");  // (posterior_cov_big_kernel: no workgroup fence, no vmcnt(0))
+    if (c + XB_NSTG - 1 < nc) stage(c + XB_NSTG - 1);
+    const int j0 = c * XB_WC;
+    if (!(live && j0 < E)) continue;  // wave-uniform: this tile's k range is done (the stores come last)
+    const uint32_t so = (uint32_t)(c % XB_NSTG) * (uint32_t)(XB_STAGE * 16);
+    const uint32_t aA = addrA + so, aB = addrB + so;
+    const int nw = min(XB_WC, E - j0);  // words of this tile in the chunk (even, wave-uniform)
+    // word j: the R^T fragment of the wave's column tile and the K fragments of its two candidate tiles, then
+    // k-blocks 2 j (chain 0) and 2 j + 1 (chain 1); the chains join the sums at the tile's chunk ends and at its
+    // extent.  Two words per iteration in register sets X and Y, each set's reads issued before the other
+    // set's MFMAs (LDS reads complete in order: lgkmcnt(3) = the older set has landed); a rolled loop, so the
+    // flush branch's paths keep the chains in the same registers (unrolled over the chunk, the merges copied
+    // MFMA results between words and waited for them every word).
+    auto mfmas = [&](const v2d& a, const v2d& b0, const v2d& b1, int j) __attribute__((always_inline)) {
+      ch[0][0] = mfma_f64(a.x, b0.x, ch[0][0]);
+      ch[1][0] = mfma_f64(a.x, b1.x, ch[1][0]);
+      ch[0][1] = mfma_f64(a.y, b0.y, ch[0][1]);
+      ch[1][1] = mfma_f64(a.y, b1.y, ch[1][1]);
+      if (--seg_left == 0 || j + 1 == E) {  // wave-uniform
+        seg_left = CW;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          sum[h] += ch[h][0] + ch[h][1];
+          ch[h][0] = ch[h][1] = d4{0.0, 0.0, 0.0, 0.0};
+        }
+      }
+    };
+    v2d xa, xb0, xb1, ya, yb0, yb1;
+    asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+                 : "=&v"(xa), "=&v"(xb0), "=&v"(xb1)
+                 : "v"(aA), "v"(aB), "i"(XB_WC * 1024)
+                 : "memory");
+#pragma unroll 1
+    for (int w = 0; w < nw; w += 2) {  // nw even
+      const uint32_t o = (uint32_t)(w + 1) * 1024u;
+      asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+                   : "=&v"(ya), "=&v"(yb0), "=&v"(yb1)
+                   : "v"(aA + o), "v"(aB + o), "i"(XB_WC * 1024)
+                   : "memory");
+      asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(xa), "+v"(xb0), "+v"(xb1));
+      mfmas(xa, xb0, xb1, j0 + w);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya), "+v"(yb0), "+v"(yb1));
+      mfmas(ya, yb0, yb1, j0 + w + 1);
+      // set X is rewritten only after set Y's MFMAs have issued: the MFMA pipe is in order, so X's MFMAs have
+      // read their operands (a rewrite right after X's own MFMAs changed results)
+      if (w + 2 < nw) {
+        const uint32_t o2 = (uint32_t)(w + 2) * 1024u;
+        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+                     : "=&v"(xa), "=&v"(xb0), "=&v"(xb1)
+                     : "v"(aA + o2), "v"(aB + o2), "i"(XB_WC * 1024)
+                     : "memory");
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (!live) return;
+  // D = R^T K^T: lane l, register r holds Q[16 ti + (l & 15)][16 tj + dr], dr = (l >> 4) + 4 r (cross_root_impl)
+  double* qout = P->q[oi];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ti = ti0 + 2 * cp + h;
+    if (ti >= RT) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int dr = mfma_drow<double>(lane, r);
+      qout[frag_index(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = sum[h][r];
+    }
+  }
 }
 
 template <int DM, class T = double>
