@@ -542,7 +542,7 @@ static bool cov_big(int N, int B, int m) {
   return N >= 128 && (size_t)((N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)) * m >= 256;
 }
 
-// The cross stage of a launch with the K(x, X) fill as 64 x 64 blocks (cross_big_kernel); DKG_CROSS_BIG=0 (A/B
+// The cross stage of a launch with the K(x, X) fill as 64 x 32 blocks (cross_big_kernel); DKG_CROSS_BIG=0 (A/B
 // measurements) keeps cross_root_plan_kernel.
 static bool cross_big() {
   static const char* env = std::getenv("DKG_CROSS_BIG");
@@ -572,7 +572,7 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
       hipLaunchKernelGGL((cross_kfill_kernel<DM>), kgrid, dim3(KF_WAVES * WAVE), 0, s, dev, xnew, B);
     }
     if constexpr (sizeof(T) == 8) {
-      if (use_kx && cross_big()) {  // K(x, X) in place: the 64 x 64 blocks, then the means and the clears
+      if (use_kx && cross_big()) {  // K(x, X) in place: the 64 x 32 blocks, then the means and the clears
         raise_lds_limit((const void*)cross_big_kernel, XB_LDS);
         hipLaunchKernelGGL(cross_big_kernel, dim3(cross_big_blocks(h.max_np, B, h.m) + pad16(B) / 16 * h.m),
                            dim3(XB_WAVES * WAVE), XB_LDS, s, dev, B, kg);
@@ -633,6 +633,8 @@ void envelope_geometry(int B, int S, int* waves_per_wg, int* split, bool narrow)
   // one group of 8 pairs meet in ordered per-pair values (envelope_body: the same bits as the wide launch).
   constexpr int ENV_MIN_WGS = 128;
   int sw = std::max(1, std::min(8, S));
+  static const char* env = std::getenv("DKG_ENV_SW");  // A/B measurements: waves per workgroup
+  if (env && std::atoi(env) >= 1) sw = std::max(1, std::min(std::atoi(env), sw));
   if (narrow && DKG_ENV_NARROW)
     while (sw > 1 && (long long)B * ((S + sw - 1) / sw) < ENV_MIN_WGS) sw = (sw + 1) / 2;
   *waves_per_wg = sw;
