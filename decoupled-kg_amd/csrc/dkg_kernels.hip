@@ -227,8 +227,9 @@ __global__ __launch_bounds__(KF_WAVES * WAVE) void cross_kfill_kernel(const Plan
 // The cross stage of a launch with the K(x, X) fill (cross_kfill_launch) in one launch: the 64 x 32 blocks of
 // Q_X (cross_big_body, the longest first), then RT x m workgroups for the means K(x, X) alpha + c and the
 // accumulator clears.  The means follow cross_root_impl's arithmetic element for element -- its fill loop's
-// per-thread fma order over the 512 threads of a row tile (thread t here runs the chains of threads t and
-// t + 256), the lane-group adds, the 8 waves in order -- so they have the bits of the one-kernel cross stage.
+// per-thread fma order over the 512 threads of a row tile (thread t here runs the chains of threads t, t + 64 W,
+// ... for W waves), the lane-group adds, the 8 waves in order -- so they have the bits of the one-kernel cross
+// stage.
 __global__ __launch_bounds__(XB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void cross_big_kernel(
     const Plan* __restrict__ P, int B, double* __restrict__ kg) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -248,10 +249,12 @@ __global__ __launch_bounds__(XB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool rv = ti * 16 + (lane & 15) < B;
   constexpr int VT = CR_WAVES * WAVE;  // the threads of cross_root_impl's fill
-  constexpr int CH = VT / (XB_WAVES * WAVE);
-  static_assert(CH == 2, "two fill chains per thread");
+  constexpr int CH = VT / (XB_WAVES * WAVE);  // fill chains per thread
+  static_assert(CH * XB_WAVES * WAVE == VT, "whole chains per thread");
   const int iters = (KB * 64 + VT - 1) / VT;
-  double mpart[CH] = {0.0, 0.0};
+  double mpart[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) mpart[c] = 0.0;
   constexpr int U = 8;  // loads issued ahead of their fmas
   for (int it0 = 0; it0 < iters; it0 += U) {
     double kv[CH][U], al[CH][U];

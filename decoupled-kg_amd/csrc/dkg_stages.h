@@ -977,9 +977,13 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
 // fetches).  Blocks of 32 columns: the longest (k = n) takes 128 words x 4 MFMAs per wave at n = 1024, so the
 // triangle's longest blocks are not the whole stage; they are dispatched first, and the candidate blocks of one
 // column block and output sit side by side on one XCD (xcd_group), sharing its R panel.
-constexpr int XB_WAVES = 4;
+#ifndef DKG_XB_WAVES
+#define DKG_XB_WAVES 4
+#endif
+constexpr int XB_WAVES = DKG_XB_WAVES;  // 4; 2 (32 x 32 blocks, twice the workgroups) was slower: stress cross
+                                        // 43.7 -> 48.6 us, headline x 10 21.2 -> 24.4 us
 constexpr int XB_TT = 2;  // column tiles of Q (row tiles of R^T) per block
-constexpr int XB_RT = 4;  // candidate tiles per block
+constexpr int XB_RT = XB_WAVES == 2 ? 2 : 4;  // candidate tiles per block
 constexpr int XB_WC = 4;  // words per staged chunk (one barrier per 16 MFMAs per wave)
 constexpr int XB_STAGE = (XB_TT + XB_RT) * XB_WC * 64;  // 16-byte words per stage buffer
 #ifndef DKG_XB_NSTG
@@ -1008,13 +1012,13 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
   if (tj0 >= T) return;  // an output with fewer training points than the widest
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int rp = wave & 1, cp = wave >> 1;  // column tile tj0 + rp; candidate tiles ti0 + 2 cp, ti0 + 2 cp + 1
+  const int rp = wave % XB_TT, cp = wave / XB_TT;  // column tile tj0 + rp; candidate tiles ti0 + 2 cp, + 1
   const double* rt = o.root_frag;
   const double* kx = P->kx[oi];
   const int W = 2 * min(tj0 + XB_TT, T);  // words the block reads: its last live column tile's k range
   const int nc = (W + XB_WC - 1) / XB_WC;
   constexpr int XB_PIECES = (XB_TT + XB_RT) * XB_WC / XB_WAVES;
-  static_assert((XB_TT + XB_RT) * XB_WC % XB_WAVES == 0 && XB_PIECES == 6, "six DMA pieces per wave per chunk");
+  static_assert((XB_TT + XB_RT) * XB_WC % XB_WAVES == 0 && (XB_PIECES == 6 || XB_PIECES == 8), "DMA pieces per wave");
   auto stage = [&](int c) {
     const int j0 = c * XB_WC, nw = min(XB_WC, W - j0);
     double2* buf = stg + (size_t)(c % XB_NSTG) * XB_STAGE;
@@ -1050,13 +1054,13 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
   for (int c = 0; c < XB_NSTG - 1; ++c)
     if (c < nc) stage(c);
   for (int c = 0; c < nc; ++c) {
-    // chunk c landed: the chunks issued after it (at most XB_NSTG - 2, six pieces each) may stay in flight
-    static_assert(XB_NSTG >= 2 && XB_NSTG <= 6, "vmcnt cases");
-    switch (min(nc - 1 - c, XB_NSTG - 2)) {  // wave-uniform
-      case 4: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-      case 3: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-      case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    // chunk c landed: the chunks issued after it (at most XB_NSTG - 2, XB_PIECES pieces each) may stay in flight
+    static_assert(XB_NSTG >= 2 && XB_NSTG <= 4, "vmcnt cases");
+    switch (min(nc - 1 - c, XB_NSTG - 2) * XB_PIECES) {  // wave-uniform
+      case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+      case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
       default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
     asm volatile("s_barrier" ::: "memory");  // (posterior_cov_big_kernel: no workgroup fence, no vmcnt(0))
