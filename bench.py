@@ -78,9 +78,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0: the process's CPU affinity (os.sched_getaffinity), capped by OMP_NUM_THREADS if set")
     ap.add_argument("--profile-reps", type=int, default=50)
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="launches in flight: launch u of an exchange period runs on stream u %% streams with its own "
-                         "plan workspace")
+                         "plan workspace (4: 10.1-10.2 M against 9.1-9.2 M with 2 at --steps 20, 15.8-16.1 M against "
+                         "15.4 M at the default; profiles/r05/streams/)")
     ap.add_argument("--batches-per-launch", type=int, default=0,
                     help="forward batches per launch (dkg_plan_forward_batches, bit-identical to one forward per "
                          "batch); 0 = auto: the largest divisor of the exchange period <= min(32, period / streams)")

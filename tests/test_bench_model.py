@@ -44,22 +44,23 @@ def test_stage_model_matches_design_table():
 
 
 def test_default_run_is_whole_graph_periods(monkeypatch):
-    """The default bench line: two launch streams, one single-stream graph per stream replayed (graph
+    """The default bench line: four launch streams, one single-stream graph per stream replayed (graph
     mode 2), a step count that is a whole number of exchange periods (no timed step falls back to eager
     launches), and batches per launch that divide the period."""
     b = _bench()
     monkeypatch.setattr("sys.argv", ["bench.py"])
     a = b.parse()
-    assert a.gpus == 1 and a.streams == 2 and a.graph == 2
+    assert a.gpus == 1 and a.streams == 4 and a.graph == 2
     assert a.steps % a.exchange_every == 0
     assert b.batches_per_launch(a.exchange_every, a) == 32
 
 
 def test_batches_per_launch_divides_the_period(monkeypatch):
     """Auto batches per launch: the largest divisor of the exchange period E that gives every stream a
-    launch of its own, at most 32 (the driver's --steps 20: E = 20, two streams of 10 batches each)."""
+    launch of its own, at most 32 (the driver's --steps 20: E = 20, four streams of 5 batches each)."""
     b = _bench()
-    for argv, E, want in ((["bench.py", "--steps", "20"], 20, 10), (["bench.py", "--streams", "4"], 256, 32),
+    for argv, E, want in ((["bench.py", "--steps", "20"], 20, 5), (["bench.py", "--streams", "2"], 20, 10),
+                          (["bench.py", "--streams", "4"], 256, 32),
                           (["bench.py", "--streams", "3"], 20, 5), (["bench.py", "--streams", "1"], 7, 7),
                           (["bench.py", "--batches-per-launch", "4"], 20, 4)):
         monkeypatch.setattr("sys.argv", argv)
