@@ -105,10 +105,14 @@ def parse():
                     help="per-kernel PMC figures per launch (tools/pmc_passes.sh + tools/pmc_report.py); auto: "
                          "profiles/r05/pmc_<workload>[_fp32].json, none if that file does not exist")
     ap.add_argument("--prep-reps", type=int, default=5, help="timed device-state preparations (0 = skip)")
-    ap.add_argument("--stress32-steps", type=int, default=8,
+    ap.add_argument("--stress32-steps", type=int, default=16,
                     help="timed forwards of the stress32 leg (BASELINE configs[4] as specified: fp32 contractions, "
                          "against the fp64 plan of the same workload; 0 = skip)")
-    ap.add_argument("--stress-steps", type=int, default=8,
+    ap.add_argument("--stress-streams", type=int, default=2,
+                    help="launch streams of the stress legs (each its own plan; eager launches): one forward's stage "
+                         "tails overlap the next one's (16 steps: 1 stream 724-731 K, 2 streams 786-814 K, 4 775-778 K "
+                         "KG-evals/s; profiles/r05/stress_streams/)")
+    ap.add_argument("--stress-steps", type=int, default=16,
                     help="timed forwards of the stress leg (BASELINE configs[4] shape, fp64; 0 = skip)")
     return ap.parse_args()
 
@@ -722,14 +726,15 @@ def main():
     stress = None
     if args.stress_steps > 0 and args.workload == "headline" and args.precision == "fp64":
         ws, ms, Ds, _, _, _, tps = setup("stress", G=1)
-        es = tps.run(1, args.stress_steps, 2, False, world)
+        es = tps.run(max(1, args.stress_streams), args.stress_steps, 2, False, world)
         fb = stage_model(ws, ws.m, [mm.num_train for mm in ms.models], Ds.shape[0], ws.B, ws.S, ws.d)
         # the stress workload's own PMC file (profiles/r05/pmc_stress.json) for its stages' traffic / busy figures
         pmc_s_path = os.path.join(PMC_DIR, "pmc_stress.json")
         pmc_s = json.load(open(pmc_s_path)) if os.path.exists(pmc_s_path) else {}
         st_s = stage_rooflines(tps.plan, tps.Xd, fb, 3, "fp64", pmc_s)
         stress = {"workload": "stress", "value": world * ws.B * args.stress_steps / es, "unit": "KG-evals/s",
-                  "steps": args.stress_steps, "ms_per_step": es / args.stress_steps * 1e3, "dtype": "f64",
+                  "steps": args.stress_steps, "streams": max(1, args.stress_streams),
+                  "ms_per_step": es / args.stress_steps * 1e3, "dtype": "f64",
                   "config": {"m": ws.m, "n_train": ws.n_train, "n_disc": Ds.shape[0], "S": ws.S, "B": ws.B,
                              "d": ws.d},
                   "stages": {k: {kk: v[kk] for kk in ("avg_launch_us", "achieved", "frac", "traffic", "valu_busy_frac",
@@ -744,7 +749,7 @@ def main():
         legs, kgs = {}, {}
         for prec in ("fp64", "fp32"):
             w3, m3, D3, _, _, _, tp3 = setup("stress32", G=1, precision=prec)
-            e3 = tp3.run(1, args.stress32_steps, 2, False, world)
+            e3 = tp3.run(max(1, args.stress_streams), args.stress32_steps, 2, False, world)
             fb3 = stage_model(w3, w3.m, [mm.num_train for mm in m3.models], D3.shape[0], w3.B, w3.S, w3.d)
             pmc3_path = os.path.join(PMC_DIR, f"pmc_stress32{'_fp32' if prec == 'fp32' else ''}.json")
             pmc3 = json.load(open(pmc3_path)) if os.path.exists(pmc3_path) else {}
@@ -763,6 +768,7 @@ def main():
         rel = ((k32 - k64).abs() / k64.abs())[keep]
         v32, v64 = legs["fp32"]["value"], legs["fp64"]["value"]
         stress32 = {"workload": "stress32", "value": v32, "unit": "KG-evals/s", "steps": args.stress32_steps,
+                    "streams": max(1, args.stress_streams),
                     "dtype": "f32 contractions (MFMA, peak 157.3 TF/s) / f64 envelope",
                     "ms_per_step": legs["fp32"]["ms_per_step"], "stages": legs["fp32"]["stages"],
                     "pmc_source": legs["fp32"]["pmc_source"], "fp64_same_workload": legs["fp64"],
