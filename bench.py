@@ -540,7 +540,9 @@ def main():
     from dkg_amd.synthetic import WORKLOADS, make_problem
     from dkg_amd.utils import sample_simplex
 
-    def setup(wname, G=None, precision=None):
+    def setup(wname, G=None, precision=None, steps=None):
+        """The workload's plan and throughput driver; `steps`: the leg's own step count, which sets its exchange
+        period (the headline's --steps for the main line)."""
         precision = precision or args.precision
         w = WORKLOADS[wname]
         model, D, X0, W = make_problem(w)
@@ -559,7 +561,7 @@ def main():
             W_local = W_all[rank::world].contiguous()
         acq = DiscreteKnowledgeGradient(model, D, W_local, target_output_ix=args.target, device=dev,
                                         precision=precision)
-        E = max(1, min(args.exchange_every, args.steps))
+        E = max(1, min(args.exchange_every, steps or args.steps))
         tp = Throughput(acq, X, w.B, E, "gather" if args.shard == "candidates" else "reduce", w.S, dev,
                         precision, G=batches_per_launch(E, args) if G is None else G)
         tp.head = args.graph_head
@@ -713,7 +715,7 @@ def main():
     # ---- non-degenerate leg: headline sizes, KG > 0 for every pair (workload headline_nd, d = 6)
     nd = None
     if args.nd_steps > 0 and args.workload == "headline" and args.precision == "fp64":
-        wn, _, Dn, _, _, _, tpn = setup("headline_nd")
+        wn, _, Dn, _, _, _, tpn = setup("headline_nd", steps=args.nd_steps)
         en = tpn.run(max(1, args.streams), args.nd_steps, min(args.warmup, 10), args.graph, world)
         env_us = tpn.plan.time_stage(tpn.Xd, 2, args.profile_reps) * 1e3
         nd = {"workload": "headline_nd", "value": world * wn.B * args.nd_steps / en, "unit": "KG-evals/s",
