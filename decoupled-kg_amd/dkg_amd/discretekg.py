@@ -98,7 +98,7 @@ def _fingerprint(obj):
     forward (``model.posterior``, discretekg.py:182-185, 275-284); the device state is rebuilt
     whenever this changes (a refit, new training data, an in-place edit)."""
     if isinstance(obj, torch.Tensor):
-        if obj.numel() <= _BY_VALUE_NUMEL and obj.device.type == "cpu":
+        if obj.is_cpu and obj.numel() <= _BY_VALUE_NUMEL:
             # hyperparameters (lengthscales, outputscale, noise, constant mean, Standardize buffers): by value,
             # since gpytorch's initialize() and constraint setters write them through .data, which does not
             # bump the version counter.  Device-resident ones are fingerprinted by identity and version only
@@ -129,7 +129,7 @@ def _weights_fingerprint(w):
     tensor (an edit through ``.data`` does not bump the version counter).  A device-resident weights tensor
     edited through ``.data`` is not seen (reading it back would cost a device synchronisation per forward):
     assign a new tensor instead."""
-    if w.device.type == "cpu" and w.numel() <= 4096:
+    if w.is_cpu and w.numel() <= 4096:
         return (id(w), w._version) + _small_values(w)
     return (id(w), w._version)
 
