@@ -86,17 +86,20 @@ constexpr int KF_WAVES = 4;
 constexpr int KF_KB = 16;  // k-blocks (of 4 columns) per fill workgroup
 
 // Pre-scaled r^2 and the kernel term exactly as cross_root_impl's fill evaluates them (same operations,
-// same order), so a loaded entry is the bits the fill would have produced.
+// same order), so a loaded entry is the bits the fill would have produced.  Compiled without FP contraction
+// (kernel_term_nc): with contraction the compiler fused differently in the fill loop and in cross_kfill_body's
+// unrolled terms, and the two gave different bits.
 template <int DM, int KIND>
 __device__ __forceinline__ double cross_kernel_term(const double (&xr)[DM], const double* __restrict__ xs_col, int d,
                                                     double os, const_dptr tab) {
+#pragma clang fp contract(off)
   double r2 = 0.0;
 #pragma unroll
   for (int k = 0; k < DM; ++k) {
     const double t = xr[k] - xs_col[min(k, d - 1)];
     r2 = fma(t, (k < d) ? t : 0.0, r2);
   }
-  return os * kernel_profile_t<KIND>(r2, tab);
+  return os * kernel_term_nc<KIND>(r2, tab);
 }
 
 // K(x_b, X_j) of output o for a row tile ti and KF_KB k-blocks, in the cross stage's B-operand order, pair-packed
@@ -118,17 +121,36 @@ __device__ __forceinline__ void cross_kfill_body(const dkg_output& o, int d, con
     xr[k] = x[(size_t)rowc * d + kk] * o.inv_lengthscale[kk];
   }
   const double os = o.outputscale;
+  // the plan's fields and every training input this thread needs, read before the first store: a store into
+  // kx may alias the plan for the compiler, which then re-read the pointers and the inputs after every store
+  // (one dependent round trip per k-block: 7 us for a launch of a few hundred thousand entries)
+  const double* __restrict__ txp = o.train_x;
+  double il[DM];
+#pragma unroll
+  for (int k = 0; k < DM; ++k) il[k] = o.inv_lengthscale[min(k, d - 1)];
+  constexpr int KPT = KF_KB / KF_WAVES;  // k-blocks per thread
+  const int kbw = kb0 + (int)(threadIdx.x >> 6);
+  double xs[KPT][DM];
+#pragma unroll
+  for (int q = 0; q < KPT; ++q) {
+    const int cc = min(4 * (kbw + KF_WAVES * q) + (lane >> 4), n - 1);
+#pragma unroll
+    for (int k = 0; k < DM; ++k) {
+      xs[q][k] = txp[(size_t)cc * d + min(k, d - 1)] * il[k];
+      asm volatile("" : "+v"(xs[q][k]));  // rounded, as cross_root_impl's LDS copy (no fma into the difference)
+    }
+  }
   auto fill = [&](auto kind_c) {
     constexpr int KIND = decltype(kind_c)::value;
     const const_dptr tab = psi_tab();
-    for (int kb = kb0 + (int)(threadIdx.x >> 6); kb < min(KB, kb0 + KF_KB); kb += KF_WAVES) {
-      const int col = 4 * kb + (lane >> 4);
-      const int cc = min(col, n - 1);
-      double xs[DM];
+    double kv[KPT];
 #pragma unroll
-      for (int k = 0; k < DM; ++k) xs[k] = o.train_x[(size_t)cc * d + min(k, d - 1)] * o.inv_lengthscale[min(k, d - 1)];
-      const double kv = cross_kernel_term<DM, KIND>(xr, xs, d, os, tab);
-      kx[frag_index(ti, kb, lane, KB)] = (rv && col < n) ? kv : 0.0;
+    for (int q = 0; q < KPT; ++q) kv[q] = cross_kernel_term<DM, KIND>(xr, xs[q], d, os, tab);
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      const int kb = kbw + KF_WAVES * q;
+      const int col = 4 * kb + (lane >> 4);
+      if (kb < min(KB, kb0 + KF_KB)) kx[frag_index(ti, kb, lane, KB)] = (rv && col < n) ? kv[q] : 0.0;
     }
   };
   switch (o.kernel) {
