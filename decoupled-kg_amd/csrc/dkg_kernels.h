@@ -41,7 +41,10 @@ __host__ __device__ inline bool cross_kfill(int np) { return DKG_CROSS_KFILL && 
 // Launches over many candidates (a launch of several forward batches, dkg_plan_forward_batches) fill K(x, X)
 // once with the separate kernel at any n: the fill replicated over the column-pair groups of a row tile (~4.5x
 // at n = 256) is then work the whole device waits on, not latency one forward hides.  Same bits either way.
-constexpr int KFILL_MIN_B = 512;
+#ifndef DKG_KFILL_MIN_B
+#define DKG_KFILL_MIN_B 512
+#endif
+constexpr int KFILL_MIN_B = DKG_KFILL_MIN_B;
 __host__ __device__ inline bool cross_kfill_launch(int np, int B) {
   return DKG_CROSS_KFILL && (np >= 512 || B >= KFILL_MIN_B);
 }
