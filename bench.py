@@ -214,6 +214,19 @@ def hip_check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed: HIP error {rc}")
 
 
+_SIDE_STREAMS = []
+
+
+def side_streams(dev, n):
+    """The launch streams besides the current one, created once and shared by every leg: HIP maps streams onto
+    the process's hardware queues (GPU_MAX_HW_QUEUES = 4) in creation order, so streams created afresh for a
+    later leg could land on the current stream's queue and serialise with it (a two-stream stress leg then ran
+    at the one-stream rate on some runs)."""
+    while len(_SIDE_STREAMS) < n:
+        _SIDE_STREAMS.append(torch.cuda.Stream(dev))
+    return _SIDE_STREAMS[:n]
+
+
 class Throughput:
     """The timed throughput path: E forward batches per exchange, ``G`` batches per launch
     (``dkg_plan_forward_batches``: one launch per stage runs G forwards, each its own B candidates and its
@@ -250,7 +263,7 @@ class Throughput:
     def run(self, ns, steps, warmup, graph, world, G=None):
         E, xchg, main_s, dev, B = self.E, self.xchg, self.main, self.dev, self.B
         G = self.G if G is None else G
-        streams = [main_s] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+        streams = [main_s] + side_streams(dev, ns - 1)
         plans = [self.acq._state.plan(self.acq._W, self.acq._target, G * B, f32=self.f32) for _ in range(ns)]
         XG = self.XG
 
