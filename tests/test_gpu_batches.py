@@ -81,3 +81,37 @@ def test_batched_launch_arguments():
     with pytest.raises(BotorchTensorDimensionError):  # DKG_ERR_ARG
         plan.forward_batches_into(X, kg, 32)               # 96 > plan capacity 64
     plan.forward_batches_into(X[:0], kg, 32)               # no batches: nothing to do
+
+
+@pytest.mark.parametrize("kernel,nu", [("matern", 2.5), ("rbf", None)])
+def test_batched_launch_outputs_of_different_sizes(kernel, nu):
+    """Outputs with different training-set sizes (ragged n: 100, 300 and 37 points) in a launch that takes the
+    K(x, X) fill and the 64 x 32 cross blocks (5 x 128 = 640 candidates), against one forward per batch (the
+    in-workgroup fill of cross_root_plan_kernel): the blocks of the smaller outputs past their own tiles return
+    early, and every output's K(x, X) uses its own k-block count."""
+    from dkg_amd.model import ModelListGPState, SingleTaskGPState
+
+    g = torch.Generator().manual_seed(5)
+    outs = []
+    for n, ls in ((100, [0.3, 0.5]), (300, [0.2, 0.4]), (37, [0.6, 0.3])):
+        X = torch.rand(n, 2, generator=g, dtype=torch.double)
+        y = torch.sin(3 * X[:, 0]) + X[:, 1] ** 2 + 0.01 * torch.randn(n, generator=g, dtype=torch.double)
+        outs.append(SingleTaskGPState(X, y, ls, 1.3, 1e-3, 0.1, kernel=kernel, nu=nu))
+    model = ModelListGPState(*outs)
+    D = torch.rand(200, 2, generator=g, dtype=torch.double)
+    W = torch.rand(6, 3, generator=g, dtype=torch.double)
+    W = W / W.sum(-1, keepdim=True)
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    B, K = 128, 5
+    X = torch.quasirandom.SobolEngine(2, scramble=True, seed=7).draw(K * B, dtype=torch.double).to(DEV)
+    big = acq._state.plan(acq._W, acq._target, K * B)
+    one = acq._state.plan(acq._W, acq._target, B)
+    kg = torch.full((K * B,), float("nan"), dtype=torch.double, device=DEV)
+    big.forward_batches_into(X, kg, B)
+    ref = torch.full_like(kg, float("nan"))
+    for j in range(K):
+        one.forward_into(X[j * B:(j + 1) * B], ref[j * B:(j + 1) * B])
+    torch.cuda.synchronize()
+    assert not torch.isnan(ref).any()
+    assert torch.equal(kg.cpu(), ref.cpu())
+    assert (ref > 0).any()
