@@ -736,7 +736,10 @@ constexpr int PB_RT = 4;  // candidate tiles per block
 constexpr int PB_CT = 4;  // line tiles per block
 constexpr int PB_WC = 2;  // words (two k-blocks each) per staged chunk; even, so chains restart in step
 constexpr int PB_STAGE = (PB_RT + PB_CT) * PB_WC * 64;  // 16-byte words per stage buffer
-constexpr int PB_NSTG = 2;                               // stage buffers: chunks in flight + the one computed
+#ifndef DKG_PB_NSTG
+#define DKG_PB_NSTG 2
+#endif
+constexpr int PB_NSTG = DKG_PB_NSTG;                               // stage buffers: chunks in flight + the one computed
 // the stage buffers, then the kernel terms (16 per lane per wave): 64 KiB, two workgroups per CU
 constexpr size_t PB_LDS = PB_NSTG * (size_t)PB_STAGE * 16 + (size_t)PB_WAVES * 16 * 64 * 8;
 
