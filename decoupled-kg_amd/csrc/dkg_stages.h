@@ -721,7 +721,7 @@ __global__ __launch_bounds__(PW_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
 // at 20 headline batches).  Here a workgroup of 4 waves (one per SIMD; two workgroups per CU, so one's
 // epilogue and chunk barriers overlap the other's MFMAs) owns a 64 x 64 block (4 candidate tiles x 4 line
 // tiles of one output); the operand tiles are staged once per workgroup through LDS in
-// chunks of PB_WC words by LDS-DMA (PB_NSTG buffers: three chunks in flight during the current one's MFMAs),
+// chunks of PB_WC words by LDS-DMA (PB_NSTG = 2 buffers: the next chunk in flight during the current one's MFMAs),
 // and each wave computes a 2 x 2 group of tiles over both halves in turn (16 accumulator chains),
 // reading its fragments from LDS with one 16-byte read per two MFMAs per operand tile.
 // 16 bytes from global memory by a global_load (address space 1), not a flat load.
