@@ -99,6 +99,8 @@ def parse():
                          "-1 = one per stream, 1 = the caller alone, in stream order)")
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")
     ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
+    ap.add_argument("--single-rank-pg", type=int, default=1,
+                    help="at one GPU, run the exchange through a one-rank RCCL process group (0: no process group)")
     ap.add_argument("--nd-steps", type=int, default=256,
                     help="timed steps of the non-degenerate headline-size leg (workload headline_nd; 0 = skip)")
     ap.add_argument("--pmc", default="auto",
@@ -519,7 +521,9 @@ def batches_per_launch(E: int, args) -> int:
     that leaves every stream a launch of its own (E / streams) and is at most 32 (a 32-batch launch of the
     headline already fills the device many times over: 8,192 envelope workgroups)."""
     if args.batches_per_launch > 0:
-        return args.batches_per_launch
+        # an explicit G applies to every leg; a leg whose exchange period it does not divide (e.g. headline_nd's
+        # E = 256 under --batches-per-launch 5) takes the largest divisor of its E below it
+        return max(g for g in range(1, min(args.batches_per_launch, E) + 1) if E % g == 0)
     cap = max(1, min(32, E // max(1, args.streams)))
     return max(g for g in range(1, cap + 1) if E % g == 0)
 
@@ -543,11 +547,21 @@ def main():
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    pg_file = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    elif args.single_rank_pg and backend == "nccl":
+        # --gpus 1: a one-rank RCCL communicator (FileStore under /tmp, no rendezvous), so the exchange after every
+        # period is the real RCCL all-reduce an N-GPU run makes and per_rank.exposed_collective_ms measures it
+        import tempfile
+
+        fd, pg_file = tempfile.mkstemp(prefix="dkg_pg1_", dir="/tmp")
+        os.close(fd)
+        os.unlink(pg_file)
+        dist.init_process_group("nccl", store=dist.FileStore(pg_file, 1), rank=0, world_size=1, device_id=dev)
 
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
@@ -855,7 +869,10 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
+    if pg_file and os.path.exists(pg_file):
+        os.unlink(pg_file)
 
 
 if __name__ == "__main__":

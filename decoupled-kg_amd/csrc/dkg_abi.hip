@@ -52,6 +52,7 @@ struct WsLayout {
   size_t q[DKG_MAX_OUTPUTS];
   size_t kx[DKG_MAX_OUTPUTS];  // 0: none (cross_kfill off for this output)
   size_t q32[DKG_MAX_OUTPUTS], root32[DKG_MAX_OUTPUTS], disc32[DKG_MAX_OUTPUTS];
+  size_t kx32[DKG_MAX_OUTPUTS];  // 0: none (F32 plans with the K(x, X) fill only)
   size_t mux[DKG_MAX_OUTPUTS];
   size_t var[DKG_MAX_OUTPUTS];
   size_t mux_all, var_all, cov_all, mu_all;
@@ -103,6 +104,11 @@ WsLayout layout(const dkg_output* outs, int m, int N, int B, int S, int d = 0, i
       off = align256(off + np * np * sizeof(float));
       L.disc32[i] = off;
       off = align256(off + (size_t)pad16(std::max(N, 1)) * np * sizeof(float));
+      L.kx32[i] = 0;
+      if (L.kx[i]) {
+        L.kx32[i] = off;
+        off = align256(off + Bp * np * sizeof(float));
+      }
     }
   }
   // contiguous blocks (the envelope stage addresses them from kernel-argument
@@ -230,6 +236,7 @@ int build_plan(const dkg_output* outs, int m, int d, const double* disc, int N, 
       P->q32[i] = reinterpret_cast<float*>(ws + L.q32[i]);
       P->root32[i] = reinterpret_cast<float*>(ws + L.root32[i]);
       P->disc32[i] = reinterpret_cast<float*>(ws + L.disc32[i]);
+      P->kx32[i] = L.kx32[i] ? reinterpret_cast<float*>(ws + L.kx32[i]) : nullptr;
     }
     P->mux[i] = reinterpret_cast<double*>(ws + L.mux[i]);
     P->var[i] = reinterpret_cast<double*>(ws + L.var[i]);
@@ -570,6 +577,11 @@ int dkg_plan_time_stage(const void* host_plan, const void* dev_plan, const doubl
 int dkg_plan_time_stage_batches(const void* host_plan, const void* dev_plan, const double* xnew, int B, int nbatch,
                                 double* kg, void* stream, int stage, int reps, float* avg_ms) {
   if (B < 1 || nbatch < 1) return fail(DKG_ERR_ARG, "B=%d nbatch=%d", B, nbatch);
+  if (!host_plan) return fail(DKG_ERR_ARG, "NULL plan pointer");
+  // (as dkg_plan_forward_batches: the product in 64 bits, so a wrapped int cannot pass the capacity check)
+  if ((long long)B * nbatch > static_cast<const Plan*>(host_plan)->max_B)
+    return fail(DKG_ERR_ARG, "%d batches of B=%d candidates > plan capacity %d", nbatch, B,
+                static_cast<const Plan*>(host_plan)->max_B);
   return time_stage(host_plan, dev_plan, xnew, B * nbatch, kg, nullptr, stream, stage, reps, avg_ms, B);
 }
 

@@ -106,6 +106,8 @@ struct Plan {
   int32_t icpt_stride;              // 64 * env_slots(N + 1): one entry per register slot of the envelope
   double* itop;                     // [S]: max_{k >= 1} a_k (-inf when N = 0)
   int* itopk;                       // [S][2]: the first k >= 1 attaining it, and how many lines do
+  float* kx32[DKG_MAX_OUTPUTS];     // F32 with the K(x, X) fill: kx's entries quad-packed in fp32 (frag32_index),
+                                    // the B operand of cross_big32_kernel (kx itself still feeds the fp64 means)
 };
 
 // By-value arguments of the state-preparation use of the cross stage.

@@ -221,7 +221,7 @@ __global__ __launch_bounds__(KF_WAVES * WAVE) void cross_kfill_kernel(const Plan
                                                                      const double* __restrict__ xnew, int B) {
   const int oi = blockIdx.z;
   if (P->kx[oi] == nullptr) return;
-  cross_kfill_body<DM>(P->o[oi], P->d, xnew, B, P->kx[oi], blockIdx.x, blockIdx.y * KF_KB);
+  cross_kfill_body<DM>(P->o[oi], P->d, xnew, B, P->kx[oi], blockIdx.x, blockIdx.y * KF_KB, P->kx32[oi]);
 }
 
 // The cross stage of a launch with the K(x, X) fill (cross_kfill_launch) in one launch: the 64 x 32 blocks of
@@ -230,6 +230,8 @@ __global__ __launch_bounds__(KF_WAVES * WAVE) void cross_kfill_kernel(const Plan
 // per-thread fma order over the 512 threads of a row tile (thread t here runs the chains of threads t, t + 64 W,
 // ... for W waves), the lane-group adds, the 8 waves in order -- so they have the bits of the one-kernel cross
 // stage.
+__device__ __forceinline__ void cross_means_body(const Plan* __restrict__ P, int B, double* __restrict__ kg, int L);
+
 __global__ __launch_bounds__(XB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void cross_big_kernel(
     const Plan* __restrict__ P, int B, double* __restrict__ kg) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -240,8 +242,27 @@ __global__ __launch_bounds__(XB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
     return;
   }
   if (DKG_ABLATIONS && (P->debug_cov & 32)) return;  // probe: the Q_X blocks alone
+  cross_means_body(P, B, kg, blockIdx.x - nbig);
+}
+
+// The fp32 plan's cross stage with the K(x, X) fill (DKG_PLAN_F32, e.g. BASELINE configs[4]): the 64 x 32 blocks
+// on fp32 MFMA (cross_big32_body), then the fp64 means and clears of cross_big_kernel.
+__global__ __launch_bounds__(XB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void cross_big32_kernel(
+    const Plan* __restrict__ P, int B, double* __restrict__ kg) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nbig = cross_big_blocks(P->max_np, B, P->m);
+  if ((int)blockIdx.x < nbig) {
+    cross_big32_body(P, B, blockIdx.x, smem);
+    return;
+  }
+  cross_means_body(P, B, kg, blockIdx.x - nbig);
+}
+
+// Means workgroup L (RT x m of them) of the big cross launches: K(x, X) alpha + c of row tile ti for output oi,
+// and the accumulator clears.
+__device__ __forceinline__ void cross_means_body(const Plan* __restrict__ P, int B, double* __restrict__ kg, int L) {
   const int RT = pad16(B) / 16;
-  const int ti = (blockIdx.x - nbig) % RT, oi = (blockIdx.x - nbig) / RT;
+  const int ti = L % RT, oi = L / RT;
   if (oi == 0) clear_tile_accumulators(P, kg, B, ti);
   const dkg_output& o = P->o[oi];
   const int n = o.n, KB = pad16(n) / 4;
@@ -536,7 +557,8 @@ static bool cov_wide(int N, int B, int m) {
   return N >= 64 && B >= 64 && (size_t)((N + 63) / 64) * ((B + 63) / 64) * m >= 512;
 }
 
-// The LDS-staged 64 x 128 blocks (posterior_cov_big_kernel: posterior_cov_kernel's bits) once a launch has at
+// The LDS-staged 64 x 64 blocks (posterior_cov_big_kernel: posterior_cov_kernel's bits; the fp32 plan's
+// posterior_cov_big32_kernel) once a launch has at
 // least one block per CU; decided on the launch's whole candidate count (a launch of several forward batches
 // takes them whatever one batch would).  DKG_COV_BIG=0 / 1 (A/B measurements) forces the choice.
 static bool cov_big(int N, int B, int m) {
@@ -574,13 +596,19 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
       dim3 kgrid(pad16(B) / 16, (h.max_np / 4 + KF_KB - 1) / KF_KB, h.m);
       hipLaunchKernelGGL((cross_kfill_kernel<DM>), kgrid, dim3(KF_WAVES * WAVE), 0, s, dev, xnew, B);
     }
-    if constexpr (sizeof(T) == 8) {
-      if (use_kx && cross_big()) {  // K(x, X) in place: the 64 x 32 blocks, then the means and the clears
+    // K(x, X) in place: the 64 x 32 blocks, then the means and the clears.  The fp32 blocks sum in another order
+    // than cross_root_plan_kernel<float>, so an F32 plan takes them only where one batch of the launch would
+    // (geom_B): a launch of several batches keeps the per-batch bits (dkg_plan_forward_batches)
+    if (use_kx && cross_big() && (sizeof(T) == 8 || cross_kfill_launch(h.max_np, geom_B))) {
+      const dim3 grid(cross_big_blocks(h.max_np, B, h.m) + pad16(B) / 16 * h.m);
+      if constexpr (sizeof(T) == 8) {
         raise_lds_limit((const void*)cross_big_kernel, XB_LDS);
-        hipLaunchKernelGGL(cross_big_kernel, dim3(cross_big_blocks(h.max_np, B, h.m) + pad16(B) / 16 * h.m),
-                           dim3(XB_WAVES * WAVE), XB_LDS, s, dev, B, kg);
-        return hipGetLastError();
+        hipLaunchKernelGGL(cross_big_kernel, grid, dim3(XB_WAVES * WAVE), XB_LDS, s, dev, B, kg);
+      } else {
+        raise_lds_limit((const void*)cross_big32_kernel, XB32_LDS);
+        hipLaunchKernelGGL(cross_big32_kernel, grid, dim3(XB_WAVES * WAVE), XB32_LDS, s, dev, B, kg);
       }
+      return hipGetLastError();
     }
     dim3 grid(pad16(B) / 16, cross_groups(h.max_np, h.d), h.m);
     const size_t lds = cross_root_lds_bytes(h.max_np, h.d);
@@ -596,6 +624,18 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
       dim3 grid(block_order_size(nbx, nby, h.m, order));
       raise_lds_limit((const void*)posterior_cov_big_kernel<DM>, PB_LDS);
       hipLaunchKernelGGL((posterior_cov_big_kernel<DM>), grid, dim3(PB_WAVES * WAVE), PB_LDS, s, dev, xnew, B,
+                         h.debug_stamp, order);
+      return hipGetLastError();
+    }
+  }
+  if constexpr (sizeof(T) == 4 && DM <= 8) {  // the fp32 plan's 64 x 64 blocks (DKG_COV_BIG32=0: A/B only)
+    static const char* env = std::getenv("DKG_COV_BIG32");
+    if (cov_big(h.N, geom_B, h.m) && (!env || std::atoi(env) != 0)) {  // (geom_B: as the cross stage above)
+      const int nbx = (h.N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
+      const int order = cov_big_order(nbx, nby, h.m);
+      dim3 grid(block_order_size(nbx, nby, h.m, order));
+      raise_lds_limit((const void*)posterior_cov_big32_kernel<DM>, PB32_LDS);
+      hipLaunchKernelGGL((posterior_cov_big32_kernel<DM>), grid, dim3(PB_WAVES * WAVE), PB32_LDS, s, dev, xnew, B,
                          h.debug_stamp, order);
       return hipGetLastError();
     }

@@ -105,9 +105,11 @@ __device__ __forceinline__ double cross_kernel_term(const double (&xr)[DM], cons
 // K(x_b, X_j) of output o for a row tile ti and KF_KB k-blocks, in the cross stage's B-operand order, pair-packed
 // (frag_index: row 16 ti + (l & 15), column 4 kb + (l >> 4); the k-blocks 2 j, 2 j + 1 of a lane in one 16-byte
 // word, as R^T's fragments, so cross_big_kernel stages both operands alike); zero outside B x n.
+// kx32 (nullable, F32 plans): the same entries rounded to fp32 and quad-packed (frag32_index), cross_big32's B operand.
 template <int DM>
 __device__ __forceinline__ void cross_kfill_body(const dkg_output& o, int d, const double* __restrict__ x, int rows,
-                                                 double* __restrict__ kx, int ti, int kb0) {
+                                                 double* __restrict__ kx, int ti, int kb0,
+                                                 float* __restrict__ kx32 = nullptr) {
   const int n = o.n;
   const int KB = pad16(n) / 4;
   const int lane = threadIdx.x & 63;
@@ -150,7 +152,11 @@ __device__ __forceinline__ void cross_kfill_body(const dkg_output& o, int d, con
     for (int q = 0; q < KPT; ++q) {
       const int kb = kbw + KF_WAVES * q;
       const int col = 4 * kb + (lane >> 4);
-      if (kb < min(KB, kb0 + KF_KB)) kx[frag_index(ti, kb, lane, KB)] = (rv && col < n) ? kv[q] : 0.0;
+      if (kb < min(KB, kb0 + KF_KB)) {
+        const double v = (rv && col < n) ? kv[q] : 0.0;
+        kx[frag_index(ti, kb, lane, KB)] = v;
+        if (kx32) kx32[frag32_index(ti, kb, lane, KB)] = (float)v;
+      }
     }
   };
   switch (o.kernel) {
@@ -731,6 +737,68 @@ __device__ __forceinline__ double2 gload_d2(const double* p) {
   return make_double2(v.x, v.y);
 }
 
+// The kernel terms s k(x_b, D_k) of a big-block wave's 2 x 2 tiles (row tiles tr, tr + 1; column tiles tc,
+// tc + 1), 16 elements per lane, parked in LDS (kvs[e * 64 + lane], e = (g * 2 + h) * 4 + r for column tile
+// tc + g, row tile tr + h and register r of the T-form MFMA's D map): evaluated while a block's first chunks
+// are in flight, so the epilogue only stores (in registers they would stay live across the contraction).
+// Returns the r^2 == 0 bits (Plan::dup), one per element.  scaled_r2_dm's and kernel_term_nc's arithmetic
+// (compiled without FP contraction, dkg_common.h), so the terms are posterior_cov_body's bits.
+template <int DM, class T>
+__device__ __forceinline__ uint32_t big_block_terms(const Plan* __restrict__ P, const dkg_output& o,
+                                                    const double* __restrict__ xnew, int B, int tr, int tc, int lane,
+                                                    double* __restrict__ kvs) {
+  const int N = P->N, d = P->d;
+  const double os = o.outputscale;
+  const int kind = o.kernel;
+  const double* __restrict__ il_p = o.inv_lengthscale;
+  const double* __restrict__ disc = P->disc;
+  uint32_t zero_r2 = 0;
+  double il[DM], xkv[2][DM];
+#pragma unroll
+  for (int c = 0; c < DM; ++c) il[c] = il_p[min(c, d - 1)];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int k = 16 * (tc + g) + (lane & 15);
+#pragma unroll
+    for (int c = 0; c < DM; ++c) xkv[g][c] = disc[(size_t)min(k, N - 1) * d + min(c, d - 1)];
+  }
+  // one covariance family per instantiation (the switch outside the 16 terms: straight-line code the
+  // scheduler interleaves) and one coefficient-table pointer for all of them
+  auto terms = [&](auto kind_c) __attribute__((always_inline)) {
+    constexpr int KIND = decltype(kind_c)::value;
+    const const_dptr tab = psi_tab();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * (tr + h) + mfma_drow<T>(lane, r);
+        double xb[DM];
+#pragma unroll
+        for (int c = 0; c < DM; ++c) xb[c] = xnew[(size_t)min(b, B - 1) * d + min(c, d - 1)];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          double r2 = 0.0;
+#pragma unroll
+          for (int c = 0; c < DM; ++c) {
+            const double t = (xb[c] - xkv[g][c]) * il[c];
+            r2 = fma(t, (c < d) ? t : 0.0, r2);
+          }
+          const double kv = os * kernel_term_nc<KIND>(r2, tab);  // rounded (stored), as posterior_cov_body
+          const int e = (g * 2 + h) * 4 + r;
+          kvs[e * 64 + lane] = kv;
+          zero_r2 |= (r2 == 0.0 ? 1u : 0u) << e;
+        }
+      }
+  };
+  switch (kind) {
+    case DKG_MATERN12: terms(std::integral_constant<int, DKG_MATERN12>{}); break;
+    case DKG_MATERN32: terms(std::integral_constant<int, DKG_MATERN32>{}); break;
+    case DKG_RBF: terms(std::integral_constant<int, DKG_RBF>{}); break;
+    default: terms(std::integral_constant<int, DKG_MATERN52>{}); break;
+  }
+  return zero_r2;
+}
+
 constexpr int PB_WAVES = 4;
 constexpr int PB_RT = 4;  // candidate tiles per block
 constexpr int PB_CT = 4;  // line tiles per block
@@ -755,7 +823,6 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   unsigned long long* st = kst_slot(dst, P, 1);
   KST_BEGIN(st);
   const dkg_output& o = P->o[oi];
-  const int d = P->d;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int rp = wave & 1, cp = wave >> 1;  // the wave's tiles: rows 2 rp, 2 rp + 1; columns 2 cp, 2 cp + 1
@@ -814,56 +881,7 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   // r^2 == 0 (Plan::dup) as one bit per element.
   const double os = o.outputscale;
   double* kvs = reinterpret_cast<double*>(stg + (size_t)PB_NSTG * PB_STAGE) + (size_t)wave * 16 * 64;
-  uint32_t zero_r2 = 0;
-  {
-    const int kind = o.kernel;
-    const double* __restrict__ il_p = o.inv_lengthscale;
-    const double* __restrict__ disc = P->disc;
-    double il[DM], xkv[2][DM];
-#pragma unroll
-    for (int c = 0; c < DM; ++c) il[c] = il_p[min(c, d - 1)];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int k = 16 * (tk0 + 2 * cp + g) + (lane & 15);
-#pragma unroll
-      for (int c = 0; c < DM; ++c) xkv[g][c] = disc[(size_t)min(k, N - 1) * d + min(c, d - 1)];
-    }
-    // one covariance family per instantiation (the switch outside the 16 terms: straight-line code the
-    // scheduler interleaves) and one coefficient-table pointer for all of them.  kernel_term_nc is compiled
-    // without FP contraction (dkg_common.h), so the terms are posterior_cov_body's bits.
-    auto terms = [&](auto kind_c) __attribute__((always_inline)) {
-      constexpr int KIND = decltype(kind_c)::value;
-      const const_dptr tab = psi_tab();
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<double>(lane, r);
-          double xb[DM];
-#pragma unroll
-          for (int c = 0; c < DM; ++c) xb[c] = xnew[(size_t)min(b, B - 1) * d + min(c, d - 1)];
-#pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            double r2 = 0.0;
-#pragma unroll
-            for (int c = 0; c < DM; ++c) {
-              const double t = (xb[c] - xkv[g][c]) * il[c];
-              r2 = fma(t, (c < d) ? t : 0.0, r2);
-            }
-            const double kv = os * kernel_term_nc<KIND>(r2, tab);  // rounded (stored), as posterior_cov_body
-            const int e = (g * 2 + h) * 4 + r;
-            kvs[e * 64 + lane] = kv;
-            zero_r2 |= (r2 == 0.0 ? 1u : 0u) << e;
-          }
-        }
-    };
-    switch (kind) {
-      case DKG_MATERN12: terms(std::integral_constant<int, DKG_MATERN12>{}); break;
-      case DKG_MATERN32: terms(std::integral_constant<int, DKG_MATERN32>{}); break;
-      case DKG_RBF: terms(std::integral_constant<int, DKG_RBF>{}); break;
-      default: terms(std::integral_constant<int, DKG_MATERN52>{}); break;
-    }
-  }
+  const uint32_t zero_r2 = big_block_terms<DM, double>(P, o, xnew, B, ti0 + 2 * rp, tk0 + 2 * cp, lane, kvs);
   KST(st, 2);
   for (int c = 0; c < nc; ++c) {
     // chunk c landed (this wave's pieces), then every wave's: the later chunks' DMAs stay in flight
@@ -942,6 +960,10 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
       word(ya0, ya1, yb0, yb1, std::integral_constant<int, 2>{});
     }
+    // Both sets' MFMAs issue here, before the next chunk's wait, barrier and fragment reads: the rewrites of
+    // sets X and Y are inline asm, which the scheduler may otherwise move the (memory-free) MFMA builtins
+    // across, and which the hazard recognizer does not see.  A scheduling barrier holds the order.
+    __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   KST(st, 3);
@@ -983,6 +1005,164 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
       q += __shfl_xor(q, 32);
       const int bb = 16 * (ti0 + 2 * rp + h) + lane;
       if (lane < 16 && bb < B) P->var[oi][bb] = os - (qh0[h] + q);
+    }
+  }
+  KST_END(st);
+}
+
+// ---------------------------------------------------------------------------
+// posterior_cov_big32_kernel (DKG_PLAN_F32, BASELINE configs[4]): posterior_cov_big_kernel's 64 x 64 blocks on
+// v_mfma_f32_16x16x4_f32.  Same block, wave and staging geometry (4 waves, each a 2 x 2 group of 16 x 16 tiles;
+// the operand panels of a block staged once by LDS-DMA; the kernel terms evaluated while the first chunks land
+// and parked in LDS), fp32 operands quad-packed (Plan::q32 / disc32: four k-blocks per 16-byte word).  An fp32
+// MFMA issues in 32 cycles against the fp64 one's 64, and a 16-byte word carries four k-blocks instead of two,
+// so a word feeds 16 MFMAs per wave at the fp64 kernel's LDS bytes per MFMA cycle: half the words, half the
+// time.  No bit-replay constraint (the fp32 plan has no other big-block path to agree with): one accumulator
+// per tile (an f32 MFMA's dependent latency, 40 cycles, is covered by the other three tiles' MFMAs), the words
+// in order, PB32_WC words per chunk (32 MFMAs per wave between barriers).  Kernel terms, subtraction and
+// variances in fp64, as posterior_cov_body<float>.
+constexpr int PB32_WC = 2;  // 16-byte words (four k-blocks each) per staged chunk
+#ifndef DKG_PB32_NSTG
+#define DKG_PB32_NSTG 3
+#endif
+constexpr int PB32_NSTG = DKG_PB32_NSTG;
+constexpr int PB32_STAGE = (PB_RT + PB_CT) * PB32_WC * 64;  // 16-byte words per stage buffer
+constexpr size_t PB32_LDS = PB32_NSTG * (size_t)PB32_STAGE * 16 + (size_t)PB_WAVES * 16 * 64 * 8;
+
+template <int DM>
+__global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_big32_kernel(
+    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst, int order) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double2* stg = reinterpret_cast<double2*>(smem);  // 16-byte words
+  const int N = P->N;
+  const int nbx = (N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
+  int bx, by, oi;
+  if (!block_order(blockIdx.x, nbx, nby, P->m, order, bx, by, oi)) return;
+  unsigned long long* st = kst_slot(dst, P, 1);
+  KST_BEGIN(st);
+  const dkg_output& o = P->o[oi];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rp = wave & 1, cp = wave >> 1;  // the wave's tiles: rows 2 rp, 2 rp + 1; columns 2 cp, 2 cp + 1
+  const int RT = pad16(B) / 16, CT = pad16(N) / 16;
+  const int KB = pad16(o.n) / 4, KP = KB / 4;  // quad words
+  const int ti0 = PB_RT * by, tk0 = PB_CT * bx;
+  const float* qx = P->q32[oi];
+  const float* qd = P->disc32[oi];
+  const int nc = (KP + PB32_WC - 1) / PB32_WC;
+  constexpr int PIECES = (PB_RT + PB_CT) * PB32_WC / PB_WAVES;
+  static_assert((PB_RT + PB_CT) * PB32_WC % PB_WAVES == 0 && PIECES == 4, "four DMA pieces per wave per chunk");
+  auto stage = [&](int c) {
+    const int j0 = c * PB32_WC, nw = min(PB32_WC, KP - j0);
+    double2* buf = stg + (size_t)(c % PB32_NSTG) * PB32_STAGE;
+#pragma unroll
+    for (int q = 0; q < PIECES; ++q) {
+      const int piece = wave + PB_WAVES * q;
+      const int t = piece / PB32_WC, w = min(piece % PB32_WC, nw - 1);
+      const float* src = t < PB_RT ? qx : qd;
+      const int tile = t < PB_RT ? min(ti0 + t, RT - 1) : min(tk0 + t - PB_RT, CT - 1);
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const void*>(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 4),
+          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(buf + piece * 64)),
+          16, 0, 0);
+    }
+  };
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
+  const uint32_t addrA = lds0 + (uint32_t)(((2 * rp) * PB32_WC) * 64 + lane) * 16;
+  const uint32_t addrB = lds0 + (uint32_t)(((PB_RT + 2 * cp) * PB32_WC) * 64 + lane) * 16;
+  const bool want_var = bx == 0 && cp == 0;  // the wave's column tiles include tile 0: its row tiles' variances
+  f4 acc[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) acc[h][g] = f4{0.f, 0.f, 0.f, 0.f};
+  double qsq[2] = {0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < PB32_NSTG - 1; ++c)
+    if (c < nc) stage(c);
+  const double os = o.outputscale;
+  double* kvs = reinterpret_cast<double*>(stg + (size_t)PB32_NSTG * PB32_STAGE) + (size_t)wave * 16 * 64;
+  const uint32_t zero_r2 = big_block_terms<DM, float>(P, o, xnew, B, ti0 + 2 * rp, tk0 + 2 * cp, lane, kvs);
+  KST(st, 2);
+  for (int c = 0; c < nc; ++c) {
+    // chunk c landed (this wave's pieces), then every wave's; the later chunks' DMAs stay in flight
+    static_assert(PB32_NSTG >= 2 && PB32_NSTG <= 3, "vmcnt cases");
+    const int later = min(nc - 1 - c, PB32_NSTG - 2);  // chunks issued after c (wave-uniform)
+    if (later >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");  // (posterior_cov_big_kernel: no workgroup fence, no vmcnt(0))
+    if (c + PB32_NSTG - 1 < nc) stage(c + PB32_NSTG - 1);
+    const uint32_t so = (uint32_t)(c % PB32_NSTG) * (uint32_t)(PB32_STAGE * 16);
+    const uint32_t aA = addrA + so, aB = addrB + so;
+    const bool two = KP - c * PB32_WC > 1;  // wave-uniform
+    v4f xa0, xa1, xb0, xb1, ya0, ya1, yb0, yb1;
+    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:%6\n\tds_read_b128 %2, %5\n\t"
+                 "ds_read_b128 %3, %5 offset:%6"
+                 : "=&v"(xa0), "=&v"(xa1), "=&v"(xb0), "=&v"(xb1)
+                 : "v"(aA), "v"(aB), "i"(PB32_WC * 1024)
+                 : "memory");
+    if (two) {
+      asm volatile("ds_read_b128 %0, %4 offset:1024\n\tds_read_b128 %1, %4 offset:%6\n\t"
+                   "ds_read_b128 %2, %5 offset:1024\n\tds_read_b128 %3, %5 offset:%6"
+                   : "=&v"(ya0), "=&v"(ya1), "=&v"(yb0), "=&v"(yb1)
+                   : "v"(aA), "v"(aB), "i"((PB32_WC + 1) * 1024)
+                   : "memory");
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
+    }
+    auto word = [&](const v4f& a0, const v4f& a1, const v4f& b0, const v4f& b1) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[0][0] = mfma_f32(a0[q], b0[q], acc[0][0]);
+        acc[0][1] = mfma_f32(a0[q], b1[q], acc[0][1]);
+        acc[1][0] = mfma_f32(a1[q], b0[q], acc[1][0]);
+        acc[1][1] = mfma_f32(a1[q], b1[q], acc[1][1]);
+      }
+      if (want_var) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          qsq[0] = fma((double)a0[q], (double)a0[q], qsq[0]);
+          qsq[1] = fma((double)a1[q], (double)a1[q], qsq[1]);
+        }
+      }
+    };
+    word(xa0, xa1, xb0, xb1);
+    if (two) {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
+      word(ya0, ya1, yb0, yb1);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the MFMAs stay ahead of the next chunk's fragment rewrites (asm)
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  KST(st, 3);
+  const int rec = cov_rec(P->m);
+  int le = lane;
+  asm volatile("" : "+v"(le));  // store addresses formed here (posterior_cov_big_kernel)
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int k = 16 * (tk0 + 2 * cp + g) + (le & 15);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<float>(le, r);
+        const int e = (g * 2 + h) * 4 + r;
+        if (b < B && k < N) {
+          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kvs[e * 64 + le] - (double)acc[h][g][r];
+          if (DKG_DUP_MARK && ((zero_r2 >> e) & 1)) atomicMin(&P->dup[b], k);  // Plan::dup
+        }
+      }
+  }
+  if (want_var) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double q = qsq[h];
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      const int bb = 16 * (ti0 + 2 * rp + h) + lane;
+      if (lane < 16 && bb < B) P->var[oi][bb] = os - q;
     }
   }
   KST_END(st);
@@ -1132,7 +1312,10 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya), "+v"(yb0), "+v"(yb1));
       mfmas(ya, yb0, yb1, j0 + w + 1);
       // set X is rewritten only after set Y's MFMAs have issued: the MFMA pipe is in order, so X's MFMAs have
-      // read their operands (a rewrite right after X's own MFMAs changed results)
+      // read their operands (a rewrite right after X's own MFMAs changed results).  The rewrite is inline asm
+      // with no data dependence on Y's MFMAs (memory-free builtins the scheduler may move across asm, and the
+      // hazard recognizer does not see into asm): a scheduling barrier holds the order.
+      __builtin_amdgcn_sched_barrier(0);
       if (w + 2 < nw) {
         const uint32_t o2 = (uint32_t)(w + 2) * 1024u;
         asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
@@ -1140,6 +1323,7 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
                      : "v"(aA + o2), "v"(aB + o2), "i"(XB_WC * 1024)
                      : "memory");
       }
+      __builtin_amdgcn_sched_barrier(0);  // (the next iteration's set-Y rewrite stays after these)
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1154,6 +1338,137 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
     for (int r = 0; r < 4; ++r) {
       const int dr = mfma_drow<double>(lane, r);
       qout[frag_index(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = sum[h][r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cross_big32 (DKG_PLAN_F32 with the K(x, X) fill): cross_big_body's 64 x 32 blocks on v_mfma_f32_16x16x4_f32,
+// R^T and K(x, X) quad-packed in fp32 (Plan::root32, Plan::kx32 written by the fill), Q_X written quad-packed
+// (Plan::q32, the covariance stage's A operand).  Column tile tj needs the words j < tj + 1 (k-blocks
+// < 4 (tj + 1): R upper triangular).  No bit-replay constraint: per candidate tile two accumulators
+// (k-block parity: an f32 MFMA's dependent latency is 40 cycles against the 32-cycle issue of the one
+// MFMA between), added at the end; XB32_WC words per chunk (32 MFMAs per wave between barriers).
+constexpr int XB32_WC = 4;
+constexpr int XB32_NSTG = 3;
+constexpr int XB32_STAGE = (XB_TT + XB_RT) * XB32_WC * 64;  // 16-byte words per stage buffer
+constexpr size_t XB32_LDS = XB32_NSTG * (size_t)XB32_STAGE * 16;
+
+__device__ __forceinline__ void cross_big32_body(const Plan* __restrict__ P, int B, int L, double* smem) {
+  static_assert(XB_WAVES == 4 && XB_RT == 4, "the fp32 blocks keep the fp64 blocks' 4-wave geometry");
+  double2* stg = reinterpret_cast<double2*>(smem);
+  const int m = P->m;
+  const int RT = pad16(B) / 16, nbi = (RT + XB_RT - 1) / XB_RT;
+  const int nbj = (P->max_np / 16 + XB_TT - 1) / XB_TT;
+  int blk, bi;
+  if (!xcd_group(L, nbj * m, nbi, blk, bi)) return;
+  const int bj = nbj - 1 - blk / m, oi = blk % m;
+  const dkg_output& o = P->o[oi];
+  const int np = pad16(o.n), T = np / 16, KB = np / 4, KP = KB / 4;
+  const int tj0 = XB_TT * bj, ti0 = XB_RT * bi;
+  if (tj0 >= T) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rp = wave % XB_TT, cp = wave / XB_TT;  // column tile tj0 + rp; candidate tiles ti0 + 2 cp, + 1
+  const float* rt = P->root32[oi];
+  const float* kx = P->kx32[oi];
+  const int W = min(tj0 + XB_TT, T);  // quad words the block reads: its last live column tile's k range
+  const int nc = (W + XB32_WC - 1) / XB32_WC;
+  constexpr int PIECES = (XB_TT + XB_RT) * XB32_WC / XB_WAVES;
+  static_assert(PIECES == 6, "six DMA pieces per wave per chunk");
+  auto stage = [&](int c) {
+    const int j0 = c * XB32_WC, nw = min(XB32_WC, W - j0);
+    double2* buf = stg + (size_t)(c % XB32_NSTG) * XB32_STAGE;
+#pragma unroll
+    for (int q = 0; q < PIECES; ++q) {
+      const int piece = wave + XB_WAVES * q;
+      const int t = piece / XB32_WC, w = min(piece % XB32_WC, nw - 1);
+      const float* src = t < XB_TT ? rt : kx;
+      const int tile = t < XB_TT ? min(tj0 + t, T - 1) : min(ti0 + t - XB_TT, RT - 1);
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const void*>(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 4),
+          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(buf + piece * 64)),
+          16, 0, 0);
+    }
+  };
+  const int tj = tj0 + rp;
+  const bool live = tj < T;
+  const int E = tj + 1;  // the tile's quad words
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
+  const uint32_t addrA = lds0 + (uint32_t)((rp * XB32_WC) * 64 + lane) * 16;
+  const uint32_t addrB = lds0 + (uint32_t)(((XB_TT + 2 * cp) * XB32_WC) * 64 + lane) * 16;
+  f4 ch[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) ch[h][0] = ch[h][1] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < XB32_NSTG - 1; ++c)
+    if (c < nc) stage(c);
+  for (int c = 0; c < nc; ++c) {
+    if (min(nc - 1 - c, XB32_NSTG - 2) >= 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // wave-uniform
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (c + XB32_NSTG - 1 < nc) stage(c + XB32_NSTG - 1);
+    const int j0 = c * XB32_WC;
+    if (!(live && j0 < E)) continue;  // wave-uniform: this tile's k range is done
+    const uint32_t so = (uint32_t)(c % XB32_NSTG) * (uint32_t)(XB32_STAGE * 16);
+    const int nw = min(XB32_WC, E - j0);  // wave-uniform, 1 .. XB32_WC
+    auto mfmas = [&](const v4f& a, const v4f& b0, const v4f& b1) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ch[0][q & 1] = mfma_f32(a[q], b0[q], ch[0][q & 1]);
+        ch[1][q & 1] = mfma_f32(a[q], b1[q], ch[1][q & 1]);
+      }
+    };
+    // two words per iteration in register sets X and Y (cross_big_body's order: each set's reads issued
+    // before the other set's MFMAs; LDS reads complete in order, so lgkmcnt(3) = the older set landed)
+    v4f xa, xb0, xb1, ya, yb0, yb1;
+    asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+                 : "=&v"(xa), "=&v"(xb0), "=&v"(xb1)
+                 : "v"(addrA + so), "v"(addrB + so), "i"(XB32_WC * 1024)
+                 : "memory");
+#pragma unroll 1
+    for (int w = 0; w < nw; w += 2) {
+      const bool hy = w + 1 < nw;  // wave-uniform
+      if (hy) {
+        const uint32_t o = so + (uint32_t)(w + 1) * 1024u;
+        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+                     : "=&v"(ya), "=&v"(yb0), "=&v"(yb1)
+                     : "v"(addrA + o), "v"(addrB + o), "i"(XB32_WC * 1024)
+                     : "memory");
+        asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(xa), "+v"(xb0), "+v"(xb1));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa), "+v"(xb0), "+v"(xb1));
+      }
+      mfmas(xa, xb0, xb1);
+      if (hy) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya), "+v"(yb0), "+v"(yb1));
+        mfmas(ya, yb0, yb1);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // set X is rewritten after set Y's MFMAs have issued (cross_big_body)
+      if (w + 2 < nw) {
+        const uint32_t o = so + (uint32_t)(w + 2) * 1024u;
+        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+                     : "=&v"(xa), "=&v"(xb0), "=&v"(xb1)
+                     : "v"(addrA + o), "v"(addrB + o), "i"(XB32_WC * 1024)
+                     : "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (!live) return;
+  // D = R^T K^T in the f32 D map: lane l, register r holds Q[16 ti + (l & 15)][16 tj + 4 (l >> 4) + r]
+  float* qout = P->q32[oi];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ti = ti0 + 2 * cp + h;
+    if (ti >= RT) continue;
+    const f4 s = ch[h][0] + ch[h][1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int dr = mfma_drow<float>(lane, r);
+      qout[frag32_index(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = s[r];
     }
   }
 }

@@ -62,7 +62,12 @@ def test_batches_per_launch_divides_the_period(monkeypatch):
     for argv, E, want in ((["bench.py", "--steps", "20"], 20, 5), (["bench.py", "--streams", "2"], 20, 10),
                           (["bench.py", "--streams", "4"], 256, 32),
                           (["bench.py", "--streams", "3"], 20, 5), (["bench.py", "--streams", "1"], 7, 7),
-                          (["bench.py", "--batches-per-launch", "4"], 20, 4)):
+                          (["bench.py", "--batches-per-launch", "4"], 20, 4),
+                          # an explicit G under a leg whose period it does not divide (headline_nd's E = 256 under
+                          # the driver-shaped --steps 20 --batches-per-launch 5): that leg's largest divisor below it
+                          (["bench.py", "--steps", "20", "--batches-per-launch", "5"], 256, 4),
+                          (["bench.py", "--steps", "20", "--batches-per-launch", "5"], 20, 5),
+                          (["bench.py", "--batches-per-launch", "64"], 16, 16)):
         monkeypatch.setattr("sys.argv", argv)
         a = b.parse()
         g = b.batches_per_launch(E, a)

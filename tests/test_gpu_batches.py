@@ -25,17 +25,20 @@ def _need_gpu():
         pytest.skip("no ROCm device")
 
 
-def _batched_vs_single(wname, B, K, target, on_grid=0, seed=3):
+def _batched_vs_single(wname, B, K, target, on_grid=0, seed=3, fused=False, precision="fp64"):
+    """fused: the per-batch reference plan is a DKG_PLAN_FUSED one (its forward is the one-launch kernel; the
+    batched launch runs the stage kernels).  precision "fp32": both plans DKG_PLAN_F32."""
     model, D, _, W = make_problem(WORKLOADS[wname])
-    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV)
+    acq = DiscreteKnowledgeGradient(model, D, W, target_output_ix=target, device=DEV, precision=precision)
+    f32 = precision == "fp32"
     d = D.shape[1]
     X = torch.quasirandom.SobolEngine(d, scramble=True, seed=seed).draw(K * B, dtype=torch.double)
     if on_grid:  # some candidates exactly on discretisation points, in the middle batch
         k = K // 2
         X[k * B:k * B + on_grid] = D[torch.arange(on_grid) * 7 % D.shape[0]]
     X = X.to(DEV)
-    big = acq._state.plan(acq._W, acq._target, K * B)
-    one = acq._state.plan(acq._W, acq._target, B)
+    big = acq._state.plan(acq._W, acq._target, K * B, f32=f32)
+    one = acq._state.plan(acq._W, acq._target, B, fused=fused, f32=f32)
     kg = torch.full((K * B,), float("nan"), dtype=torch.double, device=DEV)
     big.forward_batches_into(X, kg, B)
     ref = torch.full_like(kg, float("nan"))
@@ -63,6 +66,29 @@ def test_batched_launch_writes_the_per_batch_bits(wname, B, K, target, on_grid):
     assert torch.equal(kg2, ref)
     if wname != "headline" or on_grid:
         assert (ref > 0).any()
+
+
+@pytest.mark.parametrize("wname,B,K", [("headline", 128, 5), ("small", 37, 3), ("small", 1, 4)])
+def test_batched_launch_matches_a_fused_plan(wname, B, K):
+    """include/dkg.h promises the per-batch bits for a DKG_PLAN_FUSED plan too: its dkg_plan_forward is the
+    one-launch forward (dkg_fused.h), the batched launch the three stage kernels."""
+    model, D, _, W = make_problem(WORKLOADS[wname])
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    one = acq._state.plan(acq._W, acq._target, B, fused=True)
+    assert one.fused, "the reference plan must take the one-launch forward"
+    del one
+    kg, kg2, ref = _batched_vs_single(wname, B, K, None, on_grid=2 if B > 2 else 0, fused=True)
+    assert not torch.isnan(ref).any()
+    assert torch.equal(kg, ref) and torch.equal(kg2, ref)
+
+
+@pytest.mark.parametrize("wname,B,K", [("stress32", 256, 2), ("headline_nd", 128, 5)])
+def test_batched_launch_fp32_plan(wname, B, K):
+    """F32 plans keep the per-batch bits as well: a batched launch takes the fp32 block kernels
+    (posterior_cov_big32 / cross_big32) exactly where one batch would (stress32: both; headline_nd: neither)."""
+    kg, kg2, ref = _batched_vs_single(wname, B, K, None, precision="fp32")
+    assert not torch.isnan(ref).any()
+    assert torch.equal(kg, ref) and torch.equal(kg2, ref)
 
 
 def test_batched_launch_stress_shape():
@@ -104,8 +130,8 @@ def test_batched_launch_outputs_of_different_sizes(kernel, nu):
     acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
     B, K = 128, 5
     X = torch.quasirandom.SobolEngine(2, scramble=True, seed=7).draw(K * B, dtype=torch.double).to(DEV)
-    big = acq._state.plan(acq._W, acq._target, K * B)
-    one = acq._state.plan(acq._W, acq._target, B)
+    big = acq._state.plan(acq._W, acq._target, K * B, f32=f32)
+    one = acq._state.plan(acq._W, acq._target, B, fused=fused, f32=f32)
     kg = torch.full((K * B,), float("nan"), dtype=torch.double, device=DEV)
     big.forward_batches_into(X, kg, B)
     ref = torch.full_like(kg, float("nan"))
