@@ -37,6 +37,22 @@ struct Outputs {
   dkg_output o[DKG_MAX_OUTPUTS];
 };
 
+// One LDS-DMA piece hidden from hipcc (cdna_hip_programming.md "What hipcc does not do", LDS-DMA recipe): 16 bytes
+// per lane from gsrc into LDS at lds_dst + 16 lane (lds_dst wave-uniform, the LDS byte address).  The staged
+// big-block kernels issue their panels with it and read them with plain (compiler-counted) LDS loads: hipcc then
+// places every lgkmcnt wait before the registers' first use itself, and since it does not see the DMA it does not
+// drain every DMA in flight (vmcnt(0)) before those loads, as it does after __builtin_amdgcn_global_load_lds.  The
+// caller counts the DMA (s_waitcnt vmcnt(N) in asm), then passes a barrier, before reading the bytes.  (ds_reads in
+// inline asm with a separate wait had left the allocator free to copy the destination registers before the data
+// landed: the NaNs of the first fp32 block kernels)  M0 is written and restored in the statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+               : "memory");
+}
+
 // One v_mfma_f64_16x16x4_f64.  Lane maps (CDNA4, f64 form):
 //   A (16x4): lane l holds A[l & 15][l >> 4]
 //   B (4x16): lane l holds B[l >> 4][l & 15]

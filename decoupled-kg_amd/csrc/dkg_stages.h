@@ -1017,10 +1017,12 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
 // and parked in LDS), fp32 operands quad-packed (Plan::q32 / disc32: four k-blocks per 16-byte word).  An fp32
 // MFMA issues in 32 cycles against the fp64 one's 64, and a 16-byte word carries four k-blocks instead of two,
 // so a word feeds 16 MFMAs per wave at the fp64 kernel's LDS bytes per MFMA cycle: half the words, half the
-// time.  No bit-replay constraint (the fp32 plan has no other big-block path to agree with): one accumulator
-// per tile (an f32 MFMA's dependent latency, 40 cycles, is covered by the other three tiles' MFMAs), the words
-// in order, PB32_WC words per chunk (32 MFMAs per wave between barriers).  Kernel terms, subtraction and
-// variances in fp64, as posterior_cov_body<float>.
+// time.  No bit-replay constraint (the fp32 plan has no other big-block path to agree with): one fp32
+// accumulator per tile and chunk (an f32 MFMA's dependent latency, 40 cycles, is covered by the other three
+// tiles' MFMAs), added into fp64 sums at the next chunk's start, so only 8-term partial sums round in fp32
+// (one fp32 chain over n = 1024 terms had 3x the slope error of posterior_cov_body<float>'s eight chains).
+// The panels arrive by glds16 (hidden from hipcc) and are read with plain LDS loads.  Kernel terms,
+// subtraction and variances in fp64, as posterior_cov_body<float>.
 constexpr int PB32_WC = 2;  // 16-byte words (four k-blocks each) per staged chunk
 #ifndef DKG_PB32_NSTG
 #define DKG_PB32_NSTG 3
@@ -1033,7 +1035,8 @@ template <int DM>
 __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_big32_kernel(
     const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst, int order) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double2* stg = reinterpret_cast<double2*>(smem);  // 16-byte words
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* stg = reinterpret_cast<v4f*>(smem);  // 16-byte words
   const int N = P->N;
   const int nbx = (N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
   int bx, by, oi;
@@ -1052,31 +1055,31 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   const int nc = (KP + PB32_WC - 1) / PB32_WC;
   constexpr int PIECES = (PB_RT + PB_CT) * PB32_WC / PB_WAVES;
   static_assert((PB_RT + PB_CT) * PB32_WC % PB_WAVES == 0 && PIECES == 4, "four DMA pieces per wave per chunk");
-  auto stage = [&](int c) {
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
+  auto stage = [&](int c) {  // chunk c's panels into buffer c % PB32_NSTG (glds16: counted by vmcnt below)
     const int j0 = c * PB32_WC, nw = min(PB32_WC, KP - j0);
-    double2* buf = stg + (size_t)(c % PB32_NSTG) * PB32_STAGE;
+    const uint32_t buf = lds0 + (uint32_t)((c % PB32_NSTG) * PB32_STAGE) * 16u;
 #pragma unroll
     for (int q = 0; q < PIECES; ++q) {
       const int piece = wave + PB_WAVES * q;
       const int t = piece / PB32_WC, w = min(piece % PB32_WC, nw - 1);
       const float* src = t < PB_RT ? qx : qd;
       const int tile = t < PB_RT ? min(ti0 + t, RT - 1) : min(tk0 + t - PB_RT, CT - 1);
-      __builtin_amdgcn_global_load_lds(
-          reinterpret_cast<const void*>(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 4),
-          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(buf + piece * 64)),
-          16, 0, 0);
+      glds16(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 4, buf + (uint32_t)piece * 1024u);
     }
   };
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
-  const uint32_t addrA = lds0 + (uint32_t)(((2 * rp) * PB32_WC) * 64 + lane) * 16;
-  const uint32_t addrB = lds0 + (uint32_t)(((PB_RT + 2 * cp) * PB32_WC) * 64 + lane) * 16;
   const bool want_var = bx == 0 && cp == 0;  // the wave's column tiles include tile 0: its row tiles' variances
+  // fp32 MFMA partial sums of one chunk (8 k-blocks), added into fp64 sums at the next chunk's start (the
+  // results have long landed by then): the contraction accumulates in fp64 but for the 8-term chunk sums
   f4 acc[2][2];
+  d4 sum[2][2];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int g = 0; g < 2; ++g) acc[h][g] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < 2; ++g) {
+      acc[h][g] = f4{0.f, 0.f, 0.f, 0.f};
+      sum[h][g] = d4{0.0, 0.0, 0.0, 0.0};
+    }
   double qsq[2] = {0.0, 0.0};
 #pragma unroll
   for (int c = 0; c < PB32_NSTG - 1; ++c)
@@ -1091,51 +1094,53 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
     const int later = min(nc - 1 - c, PB32_NSTG - 2);  // chunks issued after c (wave-uniform)
     if (later >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");  // (posterior_cov_big_kernel: no workgroup fence, no vmcnt(0))
+    asm volatile("s_barrier" ::: "memory");  // (no workgroup fence: it would wait for every DMA in flight)
     if (c + PB32_NSTG - 1 < nc) stage(c + PB32_NSTG - 1);
-    const uint32_t so = (uint32_t)(c % PB32_NSTG) * (uint32_t)(PB32_STAGE * 16);
-    const uint32_t aA = addrA + so, aB = addrB + so;
-    const bool two = KP - c * PB32_WC > 1;  // wave-uniform
-    v4f xa0, xa1, xb0, xb1, ya0, ya1, yb0, yb1;
-    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:%6\n\tds_read_b128 %2, %5\n\t"
-                 "ds_read_b128 %3, %5 offset:%6"
-                 : "=&v"(xa0), "=&v"(xa1), "=&v"(xb0), "=&v"(xb1)
-                 : "v"(aA), "v"(aB), "i"(PB32_WC * 1024)
-                 : "memory");
-    if (two) {
-      asm volatile("ds_read_b128 %0, %4 offset:1024\n\tds_read_b128 %1, %4 offset:%6\n\t"
-                   "ds_read_b128 %2, %5 offset:1024\n\tds_read_b128 %3, %5 offset:%6"
-                   : "=&v"(ya0), "=&v"(ya1), "=&v"(yb0), "=&v"(yb1)
-                   : "v"(aA), "v"(aB), "i"((PB32_WC + 1) * 1024)
-                   : "memory");
-      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
-    } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
-    }
-    auto word = [&](const v4f& a0, const v4f& a1, const v4f& b0, const v4f& b1) __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[0][0] = mfma_f32(a0[q], b0[q], acc[0][0]);
-        acc[0][1] = mfma_f32(a0[q], b1[q], acc[0][1]);
-        acc[1][0] = mfma_f32(a1[q], b0[q], acc[1][0]);
-        acc[1][1] = mfma_f32(a1[q], b1[q], acc[1][1]);
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum[h][g][r] += (double)acc[h][g][r];
+        acc[h][g] = f4{0.f, 0.f, 0.f, 0.f};
       }
-      if (want_var) {
+    const v4f* bufw = stg + (size_t)(c % PB32_NSTG) * PB32_STAGE + lane;
+    const int nw = min(PB32_WC, KP - c * PB32_WC);  // wave-uniform
+    v4f fa0[PB32_WC], fa1[PB32_WC], fb0[PB32_WC], fb1[PB32_WC];  // every word read up front (slots past nw repeat a live word)
+#pragma unroll
+    for (int w = 0; w < PB32_WC; ++w) {
+      fa0[w] = bufw[((2 * rp) * PB32_WC + w) * 64];
+      fa1[w] = bufw[((2 * rp + 1) * PB32_WC + w) * 64];
+      fb0[w] = bufw[((PB_RT + 2 * cp) * PB32_WC + w) * 64];
+      fb1[w] = bufw[((PB_RT + 2 * cp + 1) * PB32_WC + w) * 64];
+    }
+#pragma unroll
+    for (int w = 0; w < PB32_WC; ++w) {
+      if (w < nw) {  // (nw < PB32_WC only for an odd word count: the last chunk)
+        const v4f a0 = fa0[w], a1 = fa1[w], b0 = fb0[w], b1 = fb1[w];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          qsq[0] = fma((double)a0[q], (double)a0[q], qsq[0]);
-          qsq[1] = fma((double)a1[q], (double)a1[q], qsq[1]);
+          acc[0][0] = mfma_f32(a0[q], b0[q], acc[0][0]);
+          acc[0][1] = mfma_f32(a0[q], b1[q], acc[0][1]);
+          acc[1][0] = mfma_f32(a1[q], b0[q], acc[1][0]);
+          acc[1][1] = mfma_f32(a1[q], b1[q], acc[1][1]);
+        }
+        if (want_var) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            qsq[0] = fma((double)a0[q], (double)a0[q], qsq[0]);
+            qsq[1] = fma((double)a1[q], (double)a1[q], qsq[1]);
+          }
         }
       }
-    };
-    word(xa0, xa1, xb0, xb1);
-    if (two) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
-      word(ya0, ya1, yb0, yb1);
     }
-    __builtin_amdgcn_sched_barrier(0);  // the MFMAs stay ahead of the next chunk's fragment rewrites (asm)
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum[h][g][r] += (double)acc[h][g][r];
   KST(st, 3);
   const int rec = cov_rec(P->m);
   int le = lane;
@@ -1150,7 +1155,7 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
         const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<float>(le, r);
         const int e = (g * 2 + h) * 4 + r;
         if (b < B && k < N) {
-          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kvs[e * 64 + le] - (double)acc[h][g][r];
+          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kvs[e * 64 + le] - sum[h][g][r];
           if (DKG_DUP_MARK && ((zero_r2 >> e) & 1)) atomicMin(&P->dup[b], k);  // Plan::dup
         }
       }
@@ -1346,9 +1351,11 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
 // cross_big32 (DKG_PLAN_F32 with the K(x, X) fill): cross_big_body's 64 x 32 blocks on v_mfma_f32_16x16x4_f32,
 // R^T and K(x, X) quad-packed in fp32 (Plan::root32, Plan::kx32 written by the fill), Q_X written quad-packed
 // (Plan::q32, the covariance stage's A operand).  Column tile tj needs the words j < tj + 1 (k-blocks
-// < 4 (tj + 1): R upper triangular).  No bit-replay constraint: per candidate tile two accumulators
-// (k-block parity: an f32 MFMA's dependent latency is 40 cycles against the 32-cycle issue of the one
-// MFMA between), added at the end; XB32_WC words per chunk (32 MFMAs per wave between barriers).
+// < 4 (tj + 1): R upper triangular).  No bit-replay constraint: per candidate tile two fp32 chains (k-block
+// parity: an f32 MFMA's dependent latency is 40 cycles against the 32-cycle issue of the one MFMA between),
+// added into fp64 sums at every chunk's start (16-term fp32 partial sums, as the split-K chunks of
+// cross_root_impl<float>); XB32_WC words per chunk (32 MFMAs per wave between barriers).  Panels by glds16,
+// read with plain LDS loads (posterior_cov_big32_kernel).
 constexpr int XB32_WC = 4;
 constexpr int XB32_NSTG = 3;
 constexpr int XB32_STAGE = (XB_TT + XB_RT) * XB32_WC * 64;  // 16-byte words per stage buffer
@@ -1356,7 +1363,8 @@ constexpr size_t XB32_LDS = XB32_NSTG * (size_t)XB32_STAGE * 16;
 
 __device__ __forceinline__ void cross_big32_body(const Plan* __restrict__ P, int B, int L, double* smem) {
   static_assert(XB_WAVES == 4 && XB_RT == 4, "the fp32 blocks keep the fp64 blocks' 4-wave geometry");
-  double2* stg = reinterpret_cast<double2*>(smem);
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* stg = reinterpret_cast<v4f*>(smem);
   const int m = P->m;
   const int RT = pad16(B) / 16, nbi = (RT + XB_RT - 1) / XB_RT;
   const int nbj = (P->max_np / 16 + XB_TT - 1) / XB_TT;
@@ -1376,31 +1384,37 @@ __device__ __forceinline__ void cross_big32_body(const Plan* __restrict__ P, int
   const int nc = (W + XB32_WC - 1) / XB32_WC;
   constexpr int PIECES = (XB_TT + XB_RT) * XB32_WC / XB_WAVES;
   static_assert(PIECES == 6, "six DMA pieces per wave per chunk");
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
   auto stage = [&](int c) {
     const int j0 = c * XB32_WC, nw = min(XB32_WC, W - j0);
-    double2* buf = stg + (size_t)(c % XB32_NSTG) * XB32_STAGE;
+    const uint32_t buf = lds0 + (uint32_t)((c % XB32_NSTG) * XB32_STAGE) * 16u;
 #pragma unroll
     for (int q = 0; q < PIECES; ++q) {
       const int piece = wave + XB_WAVES * q;
       const int t = piece / XB32_WC, w = min(piece % XB32_WC, nw - 1);
       const float* src = t < XB_TT ? rt : kx;
       const int tile = t < XB_TT ? min(tj0 + t, T - 1) : min(ti0 + t - XB_TT, RT - 1);
-      __builtin_amdgcn_global_load_lds(
-          reinterpret_cast<const void*>(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 4),
-          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(buf + piece * 64)),
-          16, 0, 0);
+      glds16(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 4, buf + (uint32_t)piece * 1024u);
     }
   };
   const int tj = tj0 + rp;
   const bool live = tj < T;
   const int E = tj + 1;  // the tile's quad words
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
-  const uint32_t addrA = lds0 + (uint32_t)((rp * XB32_WC) * 64 + lane) * 16;
-  const uint32_t addrB = lds0 + (uint32_t)(((XB_TT + 2 * cp) * XB32_WC) * 64 + lane) * 16;
   f4 ch[2][2];
+  d4 sum[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) ch[h][0] = ch[h][1] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int h = 0; h < 2; ++h) {
+    ch[h][0] = ch[h][1] = f4{0.f, 0.f, 0.f, 0.f};
+    sum[h] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  auto flush = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum[h][r] += (double)ch[h][0][r] + (double)ch[h][1][r];
+      ch[h][0] = ch[h][1] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
 #pragma unroll
   for (int c = 0; c < XB32_NSTG - 1; ++c)
     if (c < nc) stage(c);
@@ -1411,64 +1425,42 @@ __device__ __forceinline__ void cross_big32_body(const Plan* __restrict__ P, int
     if (c + XB32_NSTG - 1 < nc) stage(c + XB32_NSTG - 1);
     const int j0 = c * XB32_WC;
     if (!(live && j0 < E)) continue;  // wave-uniform: this tile's k range is done
-    const uint32_t so = (uint32_t)(c % XB32_NSTG) * (uint32_t)(XB32_STAGE * 16);
+    flush();  // the previous chunk's chains (landed long ago) into the fp64 sums
+    const v4f* bufw = stg + (size_t)(c % XB32_NSTG) * XB32_STAGE + lane;
     const int nw = min(XB32_WC, E - j0);  // wave-uniform, 1 .. XB32_WC
-    auto mfmas = [&](const v4f& a, const v4f& b0, const v4f& b1) __attribute__((always_inline)) {
+    // every word of the chunk read up front (the stage fills all XB32_WC slots, repeating a live word past the
+    // block's range, so the reads past nw are defined), the MFMAs of the tile's words only
+    v4f a[XB32_WC], b0[XB32_WC], b1[XB32_WC];
+#pragma unroll
+    for (int w = 0; w < XB32_WC; ++w) {
+      a[w] = bufw[(rp * XB32_WC + w) * 64];
+      b0[w] = bufw[((XB_TT + 2 * cp) * XB32_WC + w) * 64];
+      b1[w] = bufw[((XB_TT + 2 * cp + 1) * XB32_WC + w) * 64];
+    }
+    // words past the tile's range take a zero R^T operand (branch-free: the waits stay counted per word)
+#pragma unroll
+    for (int w = 0; w < XB32_WC; ++w) {
+      const bool lw = w < nw;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        ch[0][q & 1] = mfma_f32(a[q], b0[q], ch[0][q & 1]);
-        ch[1][q & 1] = mfma_f32(a[q], b1[q], ch[1][q & 1]);
+        const float aq = lw ? a[w][q] : 0.f;
+        ch[0][q & 1] = mfma_f32(aq, b0[w][q], ch[0][q & 1]);
+        ch[1][q & 1] = mfma_f32(aq, b1[w][q], ch[1][q & 1]);
       }
-    };
-    // two words per iteration in register sets X and Y (cross_big_body's order: each set's reads issued
-    // before the other set's MFMAs; LDS reads complete in order, so lgkmcnt(3) = the older set landed)
-    v4f xa, xb0, xb1, ya, yb0, yb1;
-    asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
-                 : "=&v"(xa), "=&v"(xb0), "=&v"(xb1)
-                 : "v"(addrA + so), "v"(addrB + so), "i"(XB32_WC * 1024)
-                 : "memory");
-#pragma unroll 1
-    for (int w = 0; w < nw; w += 2) {
-      const bool hy = w + 1 < nw;  // wave-uniform
-      if (hy) {
-        const uint32_t o = so + (uint32_t)(w + 1) * 1024u;
-        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
-                     : "=&v"(ya), "=&v"(yb0), "=&v"(yb1)
-                     : "v"(addrA + o), "v"(addrB + o), "i"(XB32_WC * 1024)
-                     : "memory");
-        asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(xa), "+v"(xb0), "+v"(xb1));
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa), "+v"(xb0), "+v"(xb1));
-      }
-      mfmas(xa, xb0, xb1);
-      if (hy) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya), "+v"(yb0), "+v"(yb1));
-        mfmas(ya, yb0, yb1);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // set X is rewritten after set Y's MFMAs have issued (cross_big_body)
-      if (w + 2 < nw) {
-        const uint32_t o = so + (uint32_t)(w + 2) * 1024u;
-        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
-                     : "=&v"(xa), "=&v"(xb0), "=&v"(xb1)
-                     : "v"(addrA + o), "v"(addrB + o), "i"(XB32_WC * 1024)
-                     : "memory");
-      }
-      __builtin_amdgcn_sched_barrier(0);
     }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (!live) return;
+  flush();
   // D = R^T K^T in the f32 D map: lane l, register r holds Q[16 ti + (l & 15)][16 tj + 4 (l >> 4) + r]
   float* qout = P->q32[oi];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int ti = ti0 + 2 * cp + h;
     if (ti >= RT) continue;
-    const f4 s = ch[h][0] + ch[h][1];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int dr = mfma_drow<float>(lane, r);
-      qout[frag32_index(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = s[r];
+      qout[frag32_index(ti, 4 * tj + (dr >> 2), (lane & 15) | ((dr & 3) << 4), KB)] = (float)sum[h][r];
     }
   }
 }

@@ -301,7 +301,7 @@ int dkg_pwl_expectation(const double* intercepts, const double* slopes, const do
 /* The lines the plan's envelope stage builds for candidates xnew (device,
  * B x d): intercepts / slopes device [B][S][N + 1], line 0 the candidate
  * itself (discretekg.py:182-223 full, :300-321 decoupled), bit-identical to
- * the envelope's.  Runs the cross and covariance stages; fp64 plans only. */
+ * the envelope's.  Runs the cross and covariance stages (an F32 plan: its fp32 contractions). */
 int dkg_plan_lines(const void* host_plan, const void* dev_plan, const double* xnew, int B, double* intercepts,
                    double* slopes, void* stream);
 

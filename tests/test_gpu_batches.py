@@ -130,8 +130,8 @@ def test_batched_launch_outputs_of_different_sizes(kernel, nu):
     acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
     B, K = 128, 5
     X = torch.quasirandom.SobolEngine(2, scramble=True, seed=7).draw(K * B, dtype=torch.double).to(DEV)
-    big = acq._state.plan(acq._W, acq._target, K * B, f32=f32)
-    one = acq._state.plan(acq._W, acq._target, B, fused=fused, f32=f32)
+    big = acq._state.plan(acq._W, acq._target, K * B)
+    one = acq._state.plan(acq._W, acq._target, B)
     kg = torch.full((K * B,), float("nan"), dtype=torch.double, device=DEV)
     big.forward_batches_into(X, kg, B)
     ref = torch.full_like(kg, float("nan"))
