@@ -567,6 +567,47 @@ static bool cov_big(int N, int B, int m) {
   return N >= 128 && (size_t)((N + 16 * PB_CT - 1) / (16 * PB_CT)) * ((B + 16 * PB_RT - 1) / (16 * PB_RT)) * m >= 256;
 }
 
+// The 64 x 32 covariance blocks (posterior_cov_blk_kernel: posterior_cov_kernel's bits, three per CU) once a launch
+// has at least one per CU: they take precedence over the 64 x 64 blocks.  DKG_COV_BLK=0 / 1 (A/B) forces the choice.
+static bool cov_blk(int N, int B, int m) {
+  static const char* env = std::getenv("DKG_COV_BLK");
+  if (env) return std::atoi(env) != 0 && N >= 1;
+  // (m >= 3: the 64 x 64 blocks, 143.7 against 164 us at BASELINE configs[4]'s shape, profiles/r06/cov)
+  return m <= 2 && N >= 64 &&
+         (size_t)((N + 16 * PK_CT - 1) / (16 * PK_CT)) * ((B + 16 * PK_RT - 1) / (16 * PK_RT)) * m >= 256;
+}
+
+// The register-operand blocks (posterior_cov_reg_kernel: posterior_cov_kernel's bits, one workgroup per CU) for
+// launches of at least one block per CU: the block height RT (4 or 5 candidate tiles, 4 line tiles) whose
+// launch takes the fewest block-heights of device rounds -- ceil(blocks / 256) x RT -- (a 5-batch headline launch:
+// 256 blocks of 5 x 4 tiles, one round; 4 x 4 tiles would need two).  One 8-wave workgroup per CU.  0: not this kernel.  DKG_COV_REG=0 / 4 / 5
+// (A/B) disables it or forces RT.
+static int cov_reg_rt(int N, int B, int m) {
+  static const char* env = std::getenv("DKG_COV_REG");
+  const int force = env ? std::atoi(env) : 0;  // off unless asked for: the 64 x 64 blocks are faster at m = 3
+  if (force == 0 || N < 64) return 0;
+  auto blocks = [&](int rt) { return (size_t)((N + 63) / 64) * ((B + 16 * rt - 1) / (16 * rt)) * m; };
+  if (force == 4 || force == 5) return force;
+  if (blocks(4) < 256) return 0;
+  auto cost = [&](int rt) { return ((blocks(rt) + 255) / 256) * (size_t)rt; };
+  return cost(5) < cost(4) ? 5 : 4;
+}
+
+// posterior_cov_rec2_kernel (m = 2): blocks of RT candidate tiles x 32 lines x both outputs, the same block-height
+// choice (blocks = ceil(B / 16 RT) x ceil(N / 32)).  DKG_COV_REC2=0 / 4 / 5 (A/B) disables it or forces RT.
+static int cov_rec2_rt(int N, int B) {
+  static const char* env = std::getenv("DKG_COV_REC2");
+  const int force = env ? std::atoi(env) : -1;
+  if (force == 0 || N < 32) return 0;
+  auto blocks = [&](int rt) { return (size_t)((N + 31) / 32) * ((B + 16 * rt - 1) / (16 * rt)); };
+  if (force == 4 || force == 5) return force;
+  // one device round of blocks (one workgroup per CU): the shortest block that fits in it; launches of more
+  // take the 64 x 32 blocks, whose three workgroups per CU measured faster there (profiles/r06/cov/h_*.txt)
+  if (blocks(5) <= 256 && blocks(5) > 192) return blocks(4) <= 256 ? 4 : 5;
+  if (blocks(4) <= 256 && blocks(4) > 192) return 4;
+  return 0;
+}
+
 // The cross stage of a launch with the K(x, X) fill as 64 x 32 blocks (cross_big_kernel); DKG_CROSS_BIG=0 (A/B
 // measurements) keeps cross_root_plan_kernel.
 static bool cross_big() {
@@ -618,6 +659,46 @@ static hipError_t launch_cross_cov_tt(const Plan& h, const Plan* dev, const doub
     return hipGetLastError();
   }
   if constexpr (sizeof(T) == 8 && DM <= 8) {  // (d > 8: the big blocks' kernel terms spill)
+    // both outputs' records from one workgroup (d <= 2: with the wider candidates the late kernel terms spill)
+    if (const int rt = (DM <= 2 && h.m == 2) ? cov_rec2_rt(h.N, B) : 0) {
+      const int nbx = (h.N + 31) / 32, nby = (B + 16 * rt - 1) / (16 * rt);
+      const int order = cov_big_order(nbx, nby, 1);
+      dim3 grid(block_order_size(nbx, nby, 1, order));
+      if (rt == 5) {
+        raise_lds_limit((const void*)posterior_cov_rec2_kernel<DM, 5>, cov_rec2_lds<5>());
+        hipLaunchKernelGGL((posterior_cov_rec2_kernel<DM, 5>), grid, dim3(PR_WAVES * WAVE), cov_rec2_lds<5>(), s,
+                           dev, xnew, B, h.debug_stamp, order);
+      } else {
+        raise_lds_limit((const void*)posterior_cov_rec2_kernel<DM, 4>, cov_rec2_lds<4>());
+        hipLaunchKernelGGL((posterior_cov_rec2_kernel<DM, 4>), grid, dim3(PR_WAVES * WAVE), cov_rec2_lds<4>(), s,
+                           dev, xnew, B, h.debug_stamp, order);
+      }
+      return hipGetLastError();
+    }
+    if (const int rt = cov_reg_rt(h.N, B, h.m)) {
+      const int nbx = (h.N + 63) / 64, nby = (B + 16 * rt - 1) / (16 * rt);
+      const int order = cov_big_order(nbx, nby, h.m);
+      dim3 grid(block_order_size(nbx, nby, h.m, order));
+      if (rt == 5) {
+        raise_lds_limit((const void*)posterior_cov_reg_kernel<DM, 5>, cov_reg_lds<5>());
+        hipLaunchKernelGGL((posterior_cov_reg_kernel<DM, 5>), grid, dim3(PR_WAVES * WAVE), cov_reg_lds<5>(), s, dev,
+                           xnew, B, h.debug_stamp, order);
+      } else {
+        raise_lds_limit((const void*)posterior_cov_reg_kernel<DM, 4>, cov_reg_lds<4>());
+        hipLaunchKernelGGL((posterior_cov_reg_kernel<DM, 4>), grid, dim3(PR_WAVES * WAVE), cov_reg_lds<4>(), s, dev,
+                           xnew, B, h.debug_stamp, order);
+      }
+      return hipGetLastError();
+    }
+    if (cov_blk(h.N, B, h.m)) {
+      const int nbx = (h.N + 16 * PK_CT - 1) / (16 * PK_CT), nby = (B + 16 * PK_RT - 1) / (16 * PK_RT);
+      const int order = cov_big_order(nbx, nby, h.m);
+      dim3 grid(block_order_size(nbx, nby, h.m, order));
+      raise_lds_limit((const void*)posterior_cov_blk_kernel<DM>, PK_LDS);
+      hipLaunchKernelGGL((posterior_cov_blk_kernel<DM>), grid, dim3(PB_WAVES * WAVE), PK_LDS, s, dev, xnew, B,
+                         h.debug_stamp, order);
+      return hipGetLastError();
+    }
     if (cov_big(h.N, B, h.m)) {
       const int nbx = (h.N + 16 * PB_CT - 1) / (16 * PB_CT), nby = (B + 16 * PB_RT - 1) / (16 * PB_RT);
       const int order = cov_big_order(nbx, nby, h.m);

@@ -1011,6 +1011,629 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
 }
 
 // ---------------------------------------------------------------------------
+// posterior_cov_reg_kernel<DM, RT> (fp64): the covariance rows of launches over many candidates in blocks of RT
+// candidate tiles x 4 line tiles of one output, one workgroup of 8 waves per CU, with posterior_cov_kernel's
+// arithmetic element for element (two K halves, four k-block chains each, (c0 + c1) + (c2 + c3), half 0 + half 1;
+// the variance per half, xor-16 / xor-32, half 0 + half 1).  Wave w owns line tile w & 3 and K half w >> 2 (the
+// two waves of a SIMD run the two halves of one line tile): its Q_D fragments are its own, the RT candidate tiles'
+// Q_X fragments are read by the four waves of its half at about the same time (one L2 read per CU, the rest from
+// L1).  No LDS staging and no barrier in the contraction: every operand goes global -> registers one word ahead,
+// 4 RT independent chains per wave and the partner wave on the SIMD hide the latencies.  The halves meet in LDS
+// at the end, each wave finalising part of the block (a sum of two addends commutes: the same bits whichever
+// adds).  RT picks the block height that fills the device in whole rounds (cov_reg_rt): a 5-batch headline
+// launch (40 candidate tiles, 64 line tiles, 2 outputs) is exactly 256 blocks of 5 x 4 tiles, where 64 x 64
+// blocks left 64 CUs with two.
+constexpr int PR_WAVES = 8;
+// row tiles finalised by half 0 (and whose kernel terms it evaluates, after its contraction in rec2): the
+// smaller share, since half 1 evaluates its terms under half 0's MFMAs
+template <int RT>
+__host__ __device__ constexpr int cov_reg_split() { return RT / 2; }
+template <int RT>
+__host__ __device__ constexpr size_t cov_reg_lds() {
+  // kernel terms [4 line tiles][RT * 4][64], exchanged half sums [4][RT * 4][64], exchanged variances [RT][16]
+  return ((size_t)4 * RT * 4 * 64 * 2 + (size_t)RT * 16) * sizeof(double);
+}
+
+template <int DM, int RT>
+__global__ __launch_bounds__(PR_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_reg_kernel(
+    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst, int order) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const int N = P->N;
+  const int nbx = (N + 63) / 64, nby = (B + 16 * RT - 1) / (16 * RT);
+  int bx, by, oi;
+  if (!block_order(blockIdx.x, nbx, nby, P->m, order, bx, by, oi)) return;
+  unsigned long long* st = kst_slot(dst, P, 1);
+  KST_BEGIN(st);
+  const dkg_output& o = P->o[oi];
+  const int d = P->d;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wl = wave & 3, half = wave >> 2;
+  constexpr int H0 = cov_reg_split<RT>();  // half 0 finalises (and evaluates the terms of) row tiles h < H0
+  const int hlo = half ? H0 : 0, hhi = half ? RT : H0;
+  const int RTt = pad16(B) / 16, CT = pad16(N) / 16;
+  const int KB = pad16(o.n) / 4, KP = KB / 2, KPs = (KP + 1) / 2;  // posterior_cov_body's halves (PC_KS = 2)
+  const int ti0 = RT * by;
+  const int tk = 4 * bx + wl;  // this wave's line tile
+  typedef const __attribute__((address_space(1))) v2d* gv2d;  // global loads (not flat)
+  gv2d ap[RT];  // lane's word-0 fragments of the candidate tiles (dead tiles read a live one)
+#pragma unroll
+  for (int h = 0; h < RT; ++h)
+    ap[h] = reinterpret_cast<gv2d>(reinterpret_cast<uintptr_t>(P->q[oi])) + ((size_t)min(ti0 + h, RTt - 1) * KP) * 64 + lane;
+  const gv2d bp =
+      reinterpret_cast<gv2d>(reinterpret_cast<uintptr_t>(o.disc_frag)) + ((size_t)min(tk, CT - 1) * KP) * 64 + lane;
+  double* kvs = smem + (size_t)wl * RT * 4 * 64;                 // kernel terms of line tile wl
+  double* xch = smem + (size_t)4 * RT * 4 * 64 + (size_t)wl * RT * 4 * 64;  // the other half's sums, line tile wl
+  double* xvar = smem + (size_t)4 * RT * 4 * 64 * 2;              // half 1's variance sums [RT][16]
+  // the kernel terms' inputs first (loads complete in order: the terms then wait for these, not the operands)
+  const double* __restrict__ il_p = o.inv_lengthscale;
+  double il[DM], xk[DM];
+  const int kcol = 16 * tk + (lane & 15);
+#pragma unroll
+  for (int c = 0; c < DM; ++c) {
+    il[c] = il_p[min(c, d - 1)];
+    xk[c] = P->disc[(size_t)min(kcol, N - 1) * d + min(c, d - 1)];
+  }
+  constexpr int HT = RT - H0 > H0 ? RT - H0 : H0;  // row tiles whose terms a wave evaluates (at most)
+  double xb[HT][4][DM];
+#pragma unroll
+  for (int u = 0; u < HT; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = min(hlo + u, RT - 1);
+      const int b = 16 * (ti0 + h) + mfma_drow<double>(lane, r);
+#pragma unroll
+      for (int c = 0; c < DM; ++c) xb[u][r][c] = xnew[(size_t)min(b, B - 1) * d + min(c, d - 1)];
+    }
+  struct Word {
+    v2d a[RT];
+    v2d b;
+  };
+  auto load = [&](Word& w, int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) w.a[h] = ap[h][(size_t)j * 64];
+    w.b = bp[(size_t)j * 64];
+  };
+  const int j0 = half ? KPs : 0, j1 = half ? KP : KPs;
+  Word w0, w1;
+  load(w0, min(j0, KP - 1));
+  // kernel terms s k(x_b, D_k) of row tiles hlo .. hhi - 1 (scaled_r2_dm's / kernel_profile's arithmetic,
+  // contraction-free), parked in LDS for the waves that finalise them
+  const double os = o.outputscale;
+  uint32_t zero_r2 = 0;  // r^2 == 0 (Plan::dup) of the terms this wave evaluates, bit (h - hlo) * 4 + r
+  {
+    auto terms = [&](auto kind_c) __attribute__((always_inline)) {
+      constexpr int KIND = decltype(kind_c)::value;
+      const const_dptr tab = psi_tab();
+#pragma unroll
+      for (int u = 0; u < HT; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double r2 = 0.0;
+#pragma unroll
+          for (int c = 0; c < DM; ++c) {
+            const double t = (xb[u][r][c] - xk[c]) * il[c];
+            r2 = fma(t, (c < d) ? t : 0.0, r2);
+          }
+          const double kv = os * kernel_term_nc<KIND>(r2, tab);  // rounded (stored)
+          if (hlo + u < hhi) {  // wave-uniform
+            kvs[((hlo + u) * 4 + r) * 64 + lane] = kv;
+            zero_r2 |= (r2 == 0.0 ? 1u : 0u) << (u * 4 + r);
+          }
+        }
+    };
+    switch (o.kernel) {
+      case DKG_MATERN12: terms(std::integral_constant<int, DKG_MATERN12>{}); break;
+      case DKG_MATERN32: terms(std::integral_constant<int, DKG_MATERN32>{}); break;
+      case DKG_RBF: terms(std::integral_constant<int, DKG_RBF>{}); break;
+      default: terms(std::integral_constant<int, DKG_MATERN52>{}); break;
+    }
+  }
+  d4 acc[RT][4];
+#pragma unroll
+  for (int h = 0; h < RT; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[h][q] = d4{0.0, 0.0, 0.0, 0.0};
+  double qsq[RT];  // every wave forms them (branch-free); line tile 0's waves use them
+#pragma unroll
+  for (int h = 0; h < RT; ++h) qsq[h] = 0.0;
+  KST(st, 2);
+  // word at relative index jr of the half: k-blocks 2 jr, 2 jr + 1 -> chains 2 (jr & 1), 2 (jr & 1) + 1
+  auto mul = [&](const Word& w, int ch) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) acc[h][ch] = mfma_f64(w.a[h].x, w.b.x, acc[h][ch]);
+#pragma unroll
+    for (int h = 0; h < RT; ++h) acc[h][ch + 1] = mfma_f64(w.a[h].y, w.b.y, acc[h][ch + 1]);
+#pragma unroll
+    for (int h = 0; h < RT; ++h) {
+      qsq[h] = fma(w.a[h].x, w.a[h].x, qsq[h]);
+      qsq[h] = fma(w.a[h].y, w.a[h].y, qsq[h]);
+    }
+  };
+  int j = j0;
+#pragma unroll 1
+  for (; j + 2 <= j1; j += 2) {
+    load(w1, j + 1);
+    mul(w0, 0);
+    load(w0, min(j + 2, KP - 1));
+    mul(w1, 2);
+  }
+  if (j < j1) mul(w0, 0);  // an odd half
+  KST(st, 3);
+  // the halves meet: each wave hands the sums of the row tiles the other half finalises to it (LDS), and the
+  // variances of line tile 0's half 1 to its half 0
+  d4 tot[RT];
+#pragma unroll
+  for (int h = 0; h < RT; ++h) {
+    tot[h] = (acc[h][0] + acc[h][1]) + (acc[h][2] + acc[h][3]);
+    if (h < hlo || h >= hhi) {  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[(h * 4 + r) * 64 + lane] = tot[h][r];
+    }
+  }
+  const bool want_var = tk == 0;
+  if (want_var && half) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) {
+      double q = qsq[h];
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (lane < 16) xvar[h * 16 + lane] = q;
+    }
+  }
+  __syncthreads();
+  const int rec = cov_rec(P->m);
+  int le = lane;
+  asm volatile("" : "+v"(le));  // store addresses formed here
+  const int k = 16 * tk + (le & 15);
+#pragma unroll
+  for (int h = 0; h < RT; ++h) {
+    if (h < hlo || h >= hhi) continue;  // wave-uniform
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = 16 * (ti0 + h) + mfma_drow<double>(le, r);
+      const double sum = tot[h][r] + xch[(h * 4 + r) * 64 + le];  // half 0 + half 1 (commutes)
+      if (b < B && k < N) {
+        const double kt = kvs[(h * 4 + r) * 64 + le];
+        P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kt - sum;
+        if (DKG_DUP_MARK && ((zero_r2 >> ((h - hlo) * 4 + r)) & 1)) atomicMin(&P->dup[b], k);  // Plan::dup
+      }
+    }
+  }
+  if (want_var && !half) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) {
+      double q = qsq[h];
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      const int bb = 16 * (ti0 + h) + lane;
+      if (lane < 16 && bb < B) P->var[oi][bb] = os - (q + xvar[h * 16 + lane]);
+    }
+  }
+  KST_END(st);
+}
+
+// ---------------------------------------------------------------------------
+// posterior_cov_rec2_kernel<DM, RT> (fp64, m = 2 outputs: the headline family): posterior_cov_reg_kernel with the
+// two outputs of a line in one workgroup, so the block's line records leave as whole 16-byte records.  Block:
+// RT candidate tiles x 2 line tiles x both outputs; wave w: line tile w & 1, output (w >> 1) & 1, K half w >> 2.
+// The halves meet in LDS as in posterior_cov_reg_kernel, the finalised values are gathered into the block's
+// record tile in LDS ([16 RT candidates][32 lines][2 outputs], 512 contiguous bytes per candidate in cov_all),
+// and the workgroup writes it with one 16-byte store per lane per two candidates: with one output per workgroup,
+// the 8-byte stores of every other record slot (16 per lane and wave) took 37 % of the block's lifetime
+// (profiles/r06/cov/covst_reg2_g5.txt).  A 5-batch headline launch is 8 x 32 = 256 blocks of 5 candidate tiles.
+template <int RT>
+__host__ __device__ constexpr size_t cov_rec2_lds() {
+  // terms [4 (line tile, output)][RT * 4][64], exchanged half sums [4][RT * 4][64], the record tile
+  // [16 RT][32][2], exchanged variances [2 outputs][RT][16]
+  return ((size_t)4 * RT * 4 * 64 * 2 + (size_t)16 * RT * 32 * 2 + (size_t)2 * RT * 16) * sizeof(double);
+}
+
+template <int DM, int RT>
+__global__ __launch_bounds__(PR_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_rec2_kernel(
+    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst, int order) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const int N = P->N;
+  const int nbx = (N + 31) / 32, nby = (B + 16 * RT - 1) / (16 * RT);
+  int bx, by, one;
+  if (!block_order(blockIdx.x, nbx, nby, 1, order, bx, by, one)) return;
+  unsigned long long* st = kst_slot(dst, P, 1);
+  KST_BEGIN(st);
+  const int d = P->d;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lt = wave & 1, oi = (wave >> 1) & 1, half = wave >> 2;
+  const int slot = wave & 3;  // (line tile, output) of the wave
+  const dkg_output& o = P->o[oi];
+  constexpr int H0 = cov_reg_split<RT>();  // half 0 finalises (and evaluates the terms of) row tiles h < H0
+  const int hlo = half ? H0 : 0, hhi = half ? RT : H0;
+  const int RTt = pad16(B) / 16, CT = pad16(N) / 16;
+  const int KB = pad16(o.n) / 4, KP = KB / 2, KPs = (KP + 1) / 2;  // posterior_cov_body's halves (PC_KS = 2)
+  const int ti0 = RT * by;
+  const int tk = 2 * bx + lt;  // this wave's line tile
+  typedef const __attribute__((address_space(1))) v2d* gv2d;  // global loads (not flat)
+  gv2d ap[RT];
+#pragma unroll
+  for (int h = 0; h < RT; ++h)
+    ap[h] = reinterpret_cast<gv2d>(reinterpret_cast<uintptr_t>(P->q[oi])) + ((size_t)min(ti0 + h, RTt - 1) * KP) * 64 + lane;
+  const gv2d bp =
+      reinterpret_cast<gv2d>(reinterpret_cast<uintptr_t>(o.disc_frag)) + ((size_t)min(tk, CT - 1) * KP) * 64 + lane;
+  double* kvs = smem + (size_t)slot * RT * 4 * 64;
+  double* xch = smem + (size_t)4 * RT * 4 * 64 + (size_t)slot * RT * 4 * 64;
+  double* rtile = smem + (size_t)4 * RT * 4 * 64 * 2;  // [16 RT][32][2]
+  double* xvar = rtile + (size_t)16 * RT * 32 * 2;     // [2][RT][16]
+  const double* __restrict__ il_p = o.inv_lengthscale;
+  double il[DM], xk[DM];
+  const int kcol = 16 * tk + (lane & 15);
+#pragma unroll
+  for (int c = 0; c < DM; ++c) {
+    il[c] = il_p[min(c, d - 1)];
+    xk[c] = P->disc[(size_t)min(kcol, N - 1) * d + min(c, d - 1)];
+  }
+  constexpr int HT = RT - H0 > H0 ? RT - H0 : H0;
+  struct Word {
+    v2d a[RT];
+    v2d b;
+  };
+  auto load = [&](Word& w, int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) w.a[h] = ap[h][(size_t)j * 64];
+    w.b = bp[(size_t)j * 64];
+  };
+  const int j0 = half ? KPs : 0, j1 = half ? KP : KPs;
+  Word w0, w1;
+  load(w0, min(j0, KP - 1));
+  const double os = o.outputscale;
+  uint32_t zero_r2 = 0;
+  // The kernel terms s k(x_b, D_k) of row tiles hlo .. hhi - 1 (scaled_r2_dm's / kernel_profile's arithmetic,
+  // contraction-free), parked in LDS for the epilogue.  Half 1's waves evaluate theirs before their contraction,
+  // half 0's after it: the two waves of a SIMD (one per half) then overlap one's VALU terms with the other's MFMAs
+  // at both ends instead of both running VALU first.
+  auto terms_of = [&]() {
+    double xb[HT][4][DM];
+#pragma unroll
+    for (int u = 0; u < HT; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = min(hlo + u, RT - 1);
+        const int b = 16 * (ti0 + h) + mfma_drow<double>(lane, r);
+#pragma unroll
+        for (int c = 0; c < DM; ++c) xb[u][r][c] = xnew[(size_t)min(b, B - 1) * d + min(c, d - 1)];
+      }
+    auto terms = [&](auto kind_c) __attribute__((always_inline)) {
+      constexpr int KIND = decltype(kind_c)::value;
+      const const_dptr tab = psi_tab();
+#pragma unroll
+      for (int u = 0; u < HT; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double r2 = 0.0;
+#pragma unroll
+          for (int c = 0; c < DM; ++c) {
+            const double t = (xb[u][r][c] - xk[c]) * il[c];
+            r2 = fma(t, (c < d) ? t : 0.0, r2);
+          }
+          const double kv = os * kernel_term_nc<KIND>(r2, tab);  // rounded (stored)
+          if (hlo + u < hhi) {  // wave-uniform
+            kvs[((hlo + u) * 4 + r) * 64 + lane] = kv;
+            zero_r2 |= (r2 == 0.0 ? 1u : 0u) << (u * 4 + r);
+          }
+        }
+    };
+    switch (o.kernel) {
+      case DKG_MATERN12: terms(std::integral_constant<int, DKG_MATERN12>{}); break;
+      case DKG_MATERN32: terms(std::integral_constant<int, DKG_MATERN32>{}); break;
+      case DKG_RBF: terms(std::integral_constant<int, DKG_RBF>{}); break;
+      default: terms(std::integral_constant<int, DKG_MATERN52>{}); break;
+    }
+  };
+  d4 acc[RT][4];
+#pragma unroll
+  for (int h = 0; h < RT; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[h][q] = d4{0.0, 0.0, 0.0, 0.0};
+  double qsq[RT];
+#pragma unroll
+  for (int h = 0; h < RT; ++h) qsq[h] = 0.0;
+  auto mul = [&](const Word& w, int ch) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) acc[h][ch] = mfma_f64(w.a[h].x, w.b.x, acc[h][ch]);
+#pragma unroll
+    for (int h = 0; h < RT; ++h) acc[h][ch + 1] = mfma_f64(w.a[h].y, w.b.y, acc[h][ch + 1]);
+#pragma unroll
+    for (int h = 0; h < RT; ++h) {
+      qsq[h] = fma(w.a[h].x, w.a[h].x, qsq[h]);
+      qsq[h] = fma(w.a[h].y, w.a[h].y, qsq[h]);
+    }
+  };
+  d4 tot[RT];  // the half's sums (c0 + c1) + (c2 + c3): formed right after the contraction, so the chains are dead
+  if (half) terms_of();  // wave-uniform
+  KST(st, 2);
+  {
+    int j = j0;
+#pragma unroll 1
+    for (; j + 2 <= j1; j += 2) {
+      load(w1, j + 1);
+      mul(w0, 0);
+      load(w0, min(j + 2, KP - 1));
+      mul(w1, 2);
+    }
+    if (j < j1) mul(w0, 0);
+  }
+#pragma unroll
+  for (int h = 0; h < RT; ++h) tot[h] = (acc[h][0] + acc[h][1]) + (acc[h][2] + acc[h][3]);
+  if (!half) terms_of();
+  KST(st, 3);
+#pragma unroll
+  for (int h = 0; h < RT; ++h) {
+    if (h < hlo || h >= hhi) {  // wave-uniform: the other half finalises this row tile
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[(h * 4 + r) * 64 + lane] = tot[h][r];
+    }
+  }
+  const bool want_var = tk == 0;
+  if (want_var && half) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) {
+      double q = qsq[h];
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (lane < 16) xvar[(oi * RT + h) * 16 + lane] = q;
+    }
+  }
+  __syncthreads();
+  // finalise: s k - (half 0 + half 1) into the record tile (candidate row 16 h + drow, line 16 lt + (l & 15))
+#pragma unroll
+  for (int h = 0; h < RT; ++h) {
+    if (h < hlo || h >= hhi) continue;  // wave-uniform
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = 16 * h + mfma_drow<double>(lane, r);
+      const double sum = tot[h][r] + xch[(h * 4 + r) * 64 + lane];  // half 0 + half 1 (commutes)
+      rtile[((size_t)rl * 32 + 16 * lt + (lane & 15)) * 2 + oi] = kvs[(h * 4 + r) * 64 + lane] - sum;
+      if (DKG_DUP_MARK && ((zero_r2 >> ((h - hlo) * 4 + r)) & 1)) {
+        const int b = 16 * (ti0 + h) + mfma_drow<double>(lane, r);
+        if (b < B && kcol < N) atomicMin(&P->dup[b], kcol);  // Plan::dup
+      }
+    }
+  }
+  if (want_var && !half) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h) {
+      double q = qsq[h];
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      const int bb = 16 * (ti0 + h) + lane;
+      if (lane < 16 && bb < B) P->var[oi][bb] = os - (q + xvar[(oi * RT + h) * 16 + lane]);
+    }
+  }
+  __syncthreads();
+  // the record tile out: lane l of a store instruction writes record (l & 31) of candidate row 2 i + (l >> 5)
+  const int k0 = 32 * bx;
+  const int kl = lane & 31;
+  const bool kin = k0 + kl < N;
+  typedef __attribute__((address_space(1))) v2d* gv2dw;
+  const v2d* rt2 = reinterpret_cast<const v2d*>(rtile);
+  for (int i = wave; i < 8 * RT; i += PR_WAVES) {
+    const int rl = 2 * i + (lane >> 5);
+    const int b = 16 * ti0 + rl;
+    if (b < B && kin) {
+      gv2dw dstp = reinterpret_cast<gv2dw>(reinterpret_cast<uintptr_t>(P->cov_all + (size_t)b * P->cov_stride)) + k0 + kl;
+      *dstp = rt2[(size_t)rl * 32 + kl];
+    }
+  }
+  KST_END(st);
+}
+
+// ---------------------------------------------------------------------------
+// posterior_cov_blk_kernel (fp64): the covariance rows of launches over many candidates (forward batches in one
+// launch, the stress shape) in 64 x 32 blocks -- 4 candidate tiles x 2 line tiles of one output -- with
+// posterior_cov_kernel's arithmetic element for element (the two K halves, four k-block chains each,
+// (c0 + c1) + (c2 + c3), half 0 + half 1; the variance sums per half, xor-16 / xor-32, half 0 + half 1), so the
+// block shape stays a speed matter.  Wave w owns candidate tile w of the block and both line tiles: 8 chains and
+// 8 kernel terms per lane, ~150 VGPRs, three workgroups per CU.  posterior_cov_big_kernel's 64 x 64 blocks
+// (234 VGPRs, two per CU) gave a 5-batch headline launch 320 workgroups for 256 CUs: the CUs holding two set the
+// stage (28 us against 19 us alone, profiles/r06/cov/covst_b1_g5.txt); 640 of these fit the device at once.
+// The operand panels arrive by glds16 (hidden from hipcc: no compiler drain of the DMAs in flight) in chunks of
+// PK_WC words, PK_NSTG buffers deep, and are read with plain LDS loads whose waits hipcc places (the inline-asm
+// reads of posterior_cov_big_kernel left the allocator free to copy their registers early); the
+// kernel terms are evaluated into registers while the first chunks land.
+constexpr int PK_RT = 4;  // candidate tiles per block (one per wave)
+constexpr int PK_CT = 2;  // line tiles per block
+#ifndef DKG_PK_WC
+#define DKG_PK_WC 2
+#endif
+constexpr int PK_WC = DKG_PK_WC;  // words (two k-blocks each) per chunk; even, so the chains restart in step
+#ifndef DKG_PK_NSTG
+#define DKG_PK_NSTG 3
+#endif
+constexpr int PK_NSTG = DKG_PK_NSTG;
+constexpr int PK_STAGE = (PK_RT + PK_CT) * PK_WC * 64;  // 16-byte words per stage buffer
+constexpr size_t PK_LDS = PK_NSTG * (size_t)PK_STAGE * 16;
+
+template <int DM>
+__global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(3))) void posterior_cov_blk_kernel(
+    const Plan* __restrict__ P, const double* __restrict__ xnew, int B, int dst, int order) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  v2d* stg = reinterpret_cast<v2d*>(smem);
+  const int N = P->N;
+  const int nbx = (N + 16 * PK_CT - 1) / (16 * PK_CT), nby = (B + 16 * PK_RT - 1) / (16 * PK_RT);
+  int bx, by, oi;
+  if (!block_order(blockIdx.x, nbx, nby, P->m, order, bx, by, oi)) return;
+  unsigned long long* st = kst_slot(dst, P, 1);
+  KST_BEGIN(st);
+  const dkg_output& o = P->o[oi];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int RT = pad16(B) / 16, CT = pad16(N) / 16;
+  const int KB = pad16(o.n) / 4, KP = KB / 2, KPs = (KP + 1) / 2;  // posterior_cov_body's halves (PC_KS = 2)
+  const int ti0 = PK_RT * by, tk0 = PK_CT * bx;
+  const int ti = ti0 + wave;  // this wave's candidate tile
+  const double* qx = P->q[oi];
+  const double* qd = o.disc_frag;
+  const int nc0 = (KPs + PK_WC - 1) / PK_WC, nc = nc0 + (KP - KPs + PK_WC - 1) / PK_WC;
+  auto chunk_start = [&](int c) { return c < nc0 ? c * PK_WC : KPs + (c - nc0) * PK_WC; };
+  auto chunk_words = [&](int c) { return c < nc0 ? min(PK_WC, KPs - c * PK_WC) : min(PK_WC, KP - chunk_start(c)); };
+  constexpr int PIECES = (PK_RT + PK_CT) * PK_WC / PB_WAVES;
+  static_assert((PK_RT + PK_CT) * PK_WC % PB_WAVES == 0 && (PIECES == 3 || PIECES == 6), "DMA pieces per wave");
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(stg);
+  auto stage = [&](int c) {  // chunk c's panels into buffer c % PK_NSTG; words past its end repeat a live word
+    const int j0 = chunk_start(c), nw = chunk_words(c);
+    const uint32_t buf = lds0 + (uint32_t)((c % PK_NSTG) * PK_STAGE) * 16u;
+#pragma unroll
+    for (int q = 0; q < PIECES; ++q) {
+      const int piece = wave + PB_WAVES * q;
+      const int t = piece / PK_WC, w = min(piece % PK_WC, nw - 1);
+      const double* src = t < PK_RT ? qx : qd;
+      const int tile = t < PK_RT ? min(ti0 + t, RT - 1) : min(tk0 + t - PK_RT, CT - 1);
+      glds16(src + (((size_t)tile * KP + j0 + w) * 64 + lane) * 2, buf + (uint32_t)piece * 1024u);
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < PK_NSTG - 1; ++c)
+    if (c < nc) stage(c);
+  // the kernel terms s k(x_b, D_k) of the wave's 8 elements per lane (big_block_terms' arithmetic), in registers
+  const double os = o.outputscale;
+  double kv[2][4];
+  uint32_t zero_r2 = 0;  // r^2 == 0 (Plan::dup), bit g * 4 + r
+  {
+    const int d = P->d;
+    const int kind = o.kernel;
+    const double* __restrict__ il_p = o.inv_lengthscale;
+    const double* __restrict__ disc = P->disc;
+    double il[DM], xkv[2][DM];
+#pragma unroll
+    for (int c = 0; c < DM; ++c) il[c] = il_p[min(c, d - 1)];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int k = 16 * (tk0 + g) + (lane & 15);
+#pragma unroll
+      for (int c = 0; c < DM; ++c) xkv[g][c] = disc[(size_t)min(k, N - 1) * d + min(c, d - 1)];
+    }
+    auto terms = [&](auto kind_c) __attribute__((always_inline)) {
+      constexpr int KIND = decltype(kind_c)::value;
+      const const_dptr tab = psi_tab();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * ti + mfma_drow<double>(lane, r);
+        double xb[DM];
+#pragma unroll
+        for (int c = 0; c < DM; ++c) xb[c] = xnew[(size_t)min(b, B - 1) * d + min(c, d - 1)];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          double r2 = 0.0;
+#pragma unroll
+          for (int c = 0; c < DM; ++c) {
+            const double t = (xb[c] - xkv[g][c]) * il[c];
+            r2 = fma(t, (c < d) ? t : 0.0, r2);
+          }
+          kv[g][r] = os * kernel_term_nc<KIND>(r2, tab);
+          asm("" : "+v"(kv[g][r]));  // rounded here, never fused into the epilogue's subtraction (posterior_cov_body)
+          zero_r2 |= (r2 == 0.0 ? 1u : 0u) << (g * 4 + r);
+        }
+      }
+    };
+    switch (kind) {
+      case DKG_MATERN12: terms(std::integral_constant<int, DKG_MATERN12>{}); break;
+      case DKG_MATERN32: terms(std::integral_constant<int, DKG_MATERN32>{}); break;
+      case DKG_RBF: terms(std::integral_constant<int, DKG_RBF>{}); break;
+      default: terms(std::integral_constant<int, DKG_MATERN52>{}); break;
+    }
+  }
+  const bool want_var = bx == 0;  // the block's line tiles include tile 0: the wave's candidates' variances
+  d4 acc[2][4], sum0[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    sum0[g] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[g][q] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  double qsq = 0.0, qh0 = 0.0;
+  KST(st, 2);
+  for (int c = 0; c < nc; ++c) {
+    static_assert(PK_NSTG >= 2 && PK_NSTG <= 3, "vmcnt cases");
+    const int later = min(nc - 1 - c, PK_NSTG - 2);  // chunks issued after c (wave-uniform)
+    if (later >= 1) {
+      if constexpr (PIECES == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");  // (no workgroup fence: it would wait for every DMA in flight)
+    if (c + PK_NSTG - 1 < nc) stage(c + PK_NSTG - 1);
+    if (c == nc0) {  // half 0 done: its sums, and the chains restart for half 1
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        sum0[g] = (acc[g][0] + acc[g][1]) + (acc[g][2] + acc[g][3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[g][q] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+      if (want_var) {
+        double q = qsq;
+        q += __shfl_xor(q, 16);
+        q += __shfl_xor(q, 32);
+        qh0 = q;
+        qsq = 0.0;
+      }
+    }
+    const v2d* bufw = stg + (size_t)(c % PK_NSTG) * PK_STAGE + lane;
+    const int nw = chunk_words(c);  // wave-uniform
+    // word w of the chunk: k-blocks 2 j, 2 j + 1 of the half (j = its word from the half's start, j = w mod 2):
+    // chains 2 (w & 1) and 2 (w & 1) + 1
+    auto word = [&](int w) __attribute__((always_inline)) {
+      const v2d a = bufw[(wave * PK_WC + w) * 64];
+      const v2d b0 = bufw[(PK_RT * PK_WC + w) * 64];
+      const v2d b1 = bufw[((PK_RT + 1) * PK_WC + w) * 64];
+      const int ch = 2 * (w & 1);
+      acc[0][ch] = mfma_f64(a.x, b0.x, acc[0][ch]);
+      acc[1][ch] = mfma_f64(a.x, b1.x, acc[1][ch]);
+      acc[0][ch + 1] = mfma_f64(a.y, b0.y, acc[0][ch + 1]);
+      acc[1][ch + 1] = mfma_f64(a.y, b1.y, acc[1][ch + 1]);
+      if (want_var) {
+        qsq = fma(a.x, a.x, qsq);
+        qsq = fma(a.y, a.y, qsq);
+      }
+    };
+    if (nw == PK_WC) {  // a whole chunk: straight-line code, hipcc interleaves the reads with the MFMAs
+#pragma unroll
+      for (int w = 0; w < PK_WC; ++w) word(w);
+    } else {
+#pragma unroll
+      for (int w = 0; w < PK_WC; ++w)
+        if (w < nw) word(w);
+    }
+  }
+  KST(st, 3);
+  const int rec = cov_rec(P->m);
+  int le = lane;
+  asm volatile("" : "+v"(le));  // store addresses formed here, not hoisted across the loop
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const d4 tot = sum0[g] + ((acc[g][0] + acc[g][1]) + (acc[g][2] + acc[g][3]));  // half 0 + half 1
+    const int k = 16 * (tk0 + g) + (le & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = 16 * ti + mfma_drow<double>(le, r);
+      if (b < B && k < N) {
+        P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kv[g][r] - tot[r];
+        if (DKG_DUP_MARK && ((zero_r2 >> (g * 4 + r)) & 1)) atomicMin(&P->dup[b], k);  // Plan::dup
+      }
+    }
+  }
+  if (want_var) {
+    double q = qsq;
+    q += __shfl_xor(q, 16);
+    q += __shfl_xor(q, 32);
+    const int bb = 16 * ti + lane;
+    if (lane < 16 && bb < B) P->var[oi][bb] = os - (qh0 + q);
+  }
+  KST_END(st);
+}
+
+// ---------------------------------------------------------------------------
 // posterior_cov_big32_kernel (DKG_PLAN_F32, BASELINE configs[4]): posterior_cov_big_kernel's 64 x 64 blocks on
 // v_mfma_f32_16x16x4_f32.  Same block, wave and staging geometry (4 waves, each a 2 x 2 group of 16 x 16 tiles;
 // the operand panels of a block staged once by LDS-DMA; the kernel terms evaluated while the first chunks land
@@ -1465,8 +2088,14 @@ __device__ __forceinline__ void cross_big32_body(const Plan* __restrict__ P, int
   }
 }
 
+// (amdgpu_waves_per_eu(4): <= 128 VGPRs, so two blocks -- or a block and an envelope workgroup -- share a CU.
+// Unconstrained, round 5's contraction-free kernel terms took it to 130 VGPRs: one block per CU, and the
+// one-forward stage went 7.32 -> 7.95 us.)
+#ifndef DKG_PC_WPE
+#define DKG_PC_WPE 4
+#endif
 template <int DM, class T = double>
-__global__ __launch_bounds__(PC_WAVES * WAVE) void posterior_cov_kernel(const Plan* __restrict__ P,
+__global__ __launch_bounds__(PC_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(DKG_PC_WPE))) void posterior_cov_kernel(const Plan* __restrict__ P,
                                                                          const double* __restrict__ xnew, int B,
                                                                          int dst) {
   __shared__ __attribute__((aligned(16))) double part[(PC_KS - 1) * 2 * PC_RB * 4 * 64];  // K-split 1.. partial tiles

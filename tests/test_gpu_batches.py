@@ -141,3 +141,39 @@ def test_batched_launch_outputs_of_different_sizes(kernel, nu):
     assert not torch.isnan(ref).any()
     assert torch.equal(kg.cpu(), ref.cpu())
     assert (ref > 0).any()
+
+
+@pytest.mark.parametrize("K,kernel,nu", [(5, "matern", 2.5), (4, "rbf", None), (5, "matern", 1.5)])
+def test_batched_launch_two_outputs_whole_records(K, kernel, nu):
+    """Two outputs of different (odd-half) training sizes, N = 1000 lines: K = 5 / 4 batches of 128 take the
+    block kernel that writes both outputs' records from one workgroup (posterior_cov_rec2_kernel, RT = 5 / 4:
+    256 blocks), whose K halves are 7 and 4 words here; its rows must be the per-batch bits (narrow blocks)."""
+    from dkg_amd.model import ModelListGPState, SingleTaskGPState
+
+    g = torch.Generator().manual_seed(11)
+    outs = []
+    for n, ls in ((100, [0.3, 0.5]), (61, [0.2, 0.4])):
+        X = torch.rand(n, 2, generator=g, dtype=torch.double)
+        y = torch.sin(3 * X[:, 0]) + X[:, 1] ** 2 + 0.01 * torch.randn(n, generator=g, dtype=torch.double)
+        outs.append(SingleTaskGPState(X, y, ls, 1.3, 1e-3, 0.1, kernel=kernel, nu=nu))
+    model = ModelListGPState(*outs)
+    D = torch.rand(1000, 2, generator=g, dtype=torch.double)
+    D[7] = torch.tensor([0.25, 0.75], dtype=torch.double)
+    W = torch.rand(8, 2, generator=g, dtype=torch.double)
+    W = W / W.sum(-1, keepdim=True)
+    acq = DiscreteKnowledgeGradient(model, D, W, device=DEV)
+    B = 128
+    X = torch.quasirandom.SobolEngine(2, scramble=True, seed=9).draw(K * B, dtype=torch.double)
+    X[130] = D[7]  # a candidate on a discretisation point (Plan::dup from the record kernel)
+    X = X.to(DEV)
+    big = acq._state.plan(acq._W, acq._target, K * B)
+    one = acq._state.plan(acq._W, acq._target, B)
+    kg = torch.full((K * B,), float("nan"), dtype=torch.double, device=DEV)
+    big.forward_batches_into(X, kg, B)
+    ref = torch.full_like(kg, float("nan"))
+    for j in range(K):
+        one.forward_into(X[j * B:(j + 1) * B], ref[j * B:(j + 1) * B])
+    torch.cuda.synchronize()
+    assert not torch.isnan(ref).any()
+    assert torch.equal(kg.cpu(), ref.cpu())
+    assert (ref > 0).any()
