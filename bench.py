@@ -100,7 +100,8 @@ def parse():
     ap.add_argument("--grad-steps", type=int, default=50, help="timed value+gradient calls at B (0 = skip)")
     ap.add_argument("--b1-calls", type=int, default=200, help="timed value+gradient calls at B = 1 (0 = skip)")
     ap.add_argument("--single-rank-pg", type=int, default=1,
-                    help="at one GPU, run the exchange through a one-rank RCCL process group (0: no process group)")
+                    help="at one GPU, time the main leg once more with a one-rank RCCL process group, its exchange a "
+                         "real all-reduce (the rccl_exchange leg; 0 = skip)")
     ap.add_argument("--nd-steps", type=int, default=256,
                     help="timed steps of the non-degenerate headline-size leg (workload headline_nd; 0 = skip)")
     ap.add_argument("--pmc", default="auto",
@@ -547,21 +548,15 @@ def main():
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # the launch streams before any process group: HIP deals its hardware queues (GPU_MAX_HW_QUEUES = 4 on the box)
+    # to streams in creation order
+    side_streams(dev, max(args.streams, args.stress_streams, 1) - 1)
     pg_file = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    elif args.single_rank_pg and backend == "nccl":
-        # --gpus 1: a one-rank RCCL communicator (FileStore under /tmp, no rendezvous), so the exchange after every
-        # period is the real RCCL all-reduce an N-GPU run makes and per_rank.exposed_collective_ms measures it
-        import tempfile
-
-        fd, pg_file = tempfile.mkstemp(prefix="dkg_pg1_", dir="/tmp")
-        os.close(fd)
-        os.unlink(pg_file)
-        dist.init_process_group("nccl", store=dist.FileStore(pg_file, 1), rank=0, world_size=1, device_id=dev)
 
     from dkg_amd import DiscreteKnowledgeGradient
     from dkg_amd.synthetic import WORKLOADS, make_problem
@@ -812,6 +807,29 @@ def main():
                             "out of reach (DESIGN.md 4.6); tests/test_gpu_parity.py::test_f32_stress32_error_model "
                             "holds every candidate to that error model instead"}
 
+    # ---- the exchange through RCCL at one GPU: a one-rank communicator (FileStore under /tmp, no rendezvous) made
+    # after every other leg, and the main leg timed again with it, so the exchange after every period is the real
+    # RCCL all-reduce an N-GPU rank makes and exposed_collective_ms measures it.  Kept out of `value`: with a
+    # process group alive the launch path measured ~10 % slower at --steps 20 (torch's RCCL watchdog thread
+    # polls the work events; profiles/r06/bench/pg_ab.txt), which is a cost of N > 1 runs, not of one GPU.
+    rccl_leg = None
+    if world == 1 and args.single_rank_pg and backend == "nccl":
+        import tempfile
+
+        fd, pg_file = tempfile.mkstemp(prefix="dkg_pg1_", dir="/tmp")
+        os.close(fd)
+        os.unlink(pg_file)
+        dist.init_process_group("nccl", store=dist.FileStore(pg_file, 1), rank=0, world_size=1, device_id=dev)
+        _, _, _, _, _, _, tpr = setup(args.workload)
+        er = tpr.run(max(1, args.streams), args.steps, args.warmup, args.graph, 1)
+        rccl_leg = {"value": w.B * args.steps / er, "unit": "KG-evals/s", "ms_per_step": er / args.steps * 1e3,
+                    "compute_ms": tpr.compute_ms, "exposed_collective_ms": tpr.exposed_ms,
+                    "exposed_frac": tpr.exposed_ms / (er * 1e3),
+                    "what": "the main leg again with a one-rank RCCL (nccl) process group: the exchange of every "
+                            f"{tpr.E}-batch period is a real RCCL all-reduce of {tpr.E} x {w.B} fp64 values; "
+                            "exposed = the final exchange nothing overlaps (what an N-GPU rank waits for at the end "
+                            "of this region)"}
+
     out = None
     if rank == 0:
         cpu = None
@@ -864,6 +882,7 @@ def main():
             "stress": stress,
             "stress32": stress32,
             "per_rank": per_rank,
+            "rccl_exchange": rccl_leg,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

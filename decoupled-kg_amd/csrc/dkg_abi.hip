@@ -746,6 +746,15 @@ int dkg_debug_read_kstamps(unsigned long long* host, int n) {
                    "hipMemcpy(stamps)");
 }
 
+int dkg_debug_cov_kernels(int mask) {
+  if (mask < 0) {
+    const int cur = set_cov_enabled(0);
+    set_cov_enabled(cur);
+    return cur;
+  }
+  return set_cov_enabled(mask);
+}
+
 int dkg_debug_wave_ops(const double* in, double* out, void* stream) {
   if (!in || !out) return fail(DKG_ERR_ARG, "NULL pointer");
   return hip_check(launch_debug_wave(in, out, (hipStream_t)stream), "debug_wave_kernel");

@@ -185,6 +185,8 @@ hipError_t launch_pwl_expectation(const double* a, const double* b, const double
 // Per-workgroup phase stamps of the forward kernels: [3 kernels][KST_WG][8].
 constexpr int KST_WG = 1024;
 hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s);
+// The opt-in fp64 covariance block kernels (dkg_debug_cov_kernels): sets the mask, returns the previous one.
+int set_cov_enabled(int mask);
 hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStream_t s);
 
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and

@@ -569,11 +569,30 @@ static bool cov_big(int N, int B, int m) {
 
 // The 64 x 32 covariance blocks (posterior_cov_blk_kernel: posterior_cov_kernel's bits, three per CU) once a launch
 // has at least one per CU: they take precedence over the 64 x 64 blocks.  DKG_COV_BLK=0 / 1 (A/B) forces the choice.
+// The opt-in covariance block kernels (bits: DKG_COV_ENABLE_BLK / _REC2 / _REG), enabled by their environment
+// variables (DKG_COV_BLK / DKG_COV_REC2 / DKG_COV_REG) or by dkg_debug_cov_kernels (tests: each gives the narrow
+// kernel's bits, checked by tests/test_gpu_batches.py with it enabled).
+static int g_cov_enable = -1;  // -1: from the environment at first use
+static int cov_enabled() {
+  if (g_cov_enable < 0) {
+    auto on = [](const char* v) { const char* e = std::getenv(v); return e && std::atoi(e) != 0; };
+    g_cov_enable = (on("DKG_COV_BLK") ? DKG_COV_ENABLE_BLK : 0) | (on("DKG_COV_REC2") ? DKG_COV_ENABLE_REC2 : 0) |
+                   (on("DKG_COV_REG") ? DKG_COV_ENABLE_REG : 0);
+  }
+  return g_cov_enable;
+}
+int set_cov_enabled(int mask) {
+  const int prev = cov_enabled();
+  g_cov_enable = mask & (DKG_COV_ENABLE_BLK | DKG_COV_ENABLE_REC2 | DKG_COV_ENABLE_REG);
+  return prev;
+}
+
+// Off unless enabled: alone a 5-batch headline launch takes 27.7 us against the 64 x 64 blocks' 31.4, but
+// with the four launch streams of bench.py the 64 x 64 blocks give the higher rate (10.0-10.4 against
+// 9.5-9.7 M KG-evals/s at --steps 20, profiles/r06/cov/covab_*.txt): with forwards in flight the rate is the
+// stages' summed CU time, not one launch's latency.  (m >= 3 alone: 164 against 143.7 us at configs[4].)
 static bool cov_blk(int N, int B, int m) {
-  static const char* env = std::getenv("DKG_COV_BLK");
-  if (env) return std::atoi(env) != 0 && N >= 1;
-  // (m >= 3: the 64 x 64 blocks, 143.7 against 164 us at BASELINE configs[4]'s shape, profiles/r06/cov)
-  return m <= 2 && N >= 64 &&
+  return (cov_enabled() & DKG_COV_ENABLE_BLK) && N >= 64 &&
          (size_t)((N + 16 * PK_CT - 1) / (16 * PK_CT)) * ((B + 16 * PK_RT - 1) / (16 * PK_RT)) * m >= 256;
 }
 
@@ -583,11 +602,9 @@ static bool cov_blk(int N, int B, int m) {
 // 256 blocks of 5 x 4 tiles, one round; 4 x 4 tiles would need two).  One 8-wave workgroup per CU.  0: not this kernel.  DKG_COV_REG=0 / 4 / 5
 // (A/B) disables it or forces RT.
 static int cov_reg_rt(int N, int B, int m) {
-  static const char* env = std::getenv("DKG_COV_REG");
-  const int force = env ? std::atoi(env) : 0;  // off unless asked for: the 64 x 64 blocks are faster at m = 3
-  if (force == 0 || N < 64) return 0;
+  // off unless enabled: the 64 x 64 blocks are faster at m = 3, and it takes a CU whole as rec2 does
+  if (!(cov_enabled() & DKG_COV_ENABLE_REG) || N < 64) return 0;
   auto blocks = [&](int rt) { return (size_t)((N + 63) / 64) * ((B + 16 * rt - 1) / (16 * rt)) * m; };
-  if (force == 4 || force == 5) return force;
   if (blocks(4) < 256) return 0;
   auto cost = [&](int rt) { return ((blocks(rt) + 255) / 256) * (size_t)rt; };
   return cost(5) < cost(4) ? 5 : 4;
@@ -595,13 +612,14 @@ static int cov_reg_rt(int N, int B, int m) {
 
 // posterior_cov_rec2_kernel (m = 2): blocks of RT candidate tiles x 32 lines x both outputs, the same block-height
 // choice (blocks = ceil(B / 16 RT) x ceil(N / 32)).  DKG_COV_REC2=0 / 4 / 5 (A/B) disables it or forces RT.
+// Off unless DKG_COV_REC2=1 (or 4 / 5 to force RT): the fastest covariance launch alone (a 5-batch headline launch
+// 23.0 us, 0.38 of the fp64 roof, against 31.4), but one 8-wave workgroup of 256 VGPRs and 121 KB of LDS takes a
+// CU whole, so nothing of the other streams' forwards runs beside it: 8.9-9.1 against 10.0-10.4 M KG-evals/s in
+// bench.py's --steps 20 line (profiles/r06/cov/covab_*.txt).
 static int cov_rec2_rt(int N, int B) {
-  static const char* env = std::getenv("DKG_COV_REC2");
-  const int force = env ? std::atoi(env) : -1;
-  if (force == 0 || N < 32) return 0;
+  if (!(cov_enabled() & DKG_COV_ENABLE_REC2) || N < 32) return 0;
   auto blocks = [&](int rt) { return (size_t)((N + 31) / 32) * ((B + 16 * rt - 1) / (16 * rt)); };
-  if (force == 4 || force == 5) return force;
-  // one device round of blocks (one workgroup per CU): the shortest block that fits in it; launches of more
+  // (on) one device round of blocks (one workgroup per CU): the shortest block that fits in it; launches of more
   // take the 64 x 32 blocks, whose three workgroups per CU measured faster there (profiles/r06/cov/h_*.txt)
   if (blocks(5) <= 256 && blocks(5) > 192) return blocks(4) <= 256 ? 4 : 5;
   if (blocks(4) <= 256 && blocks(4) > 192) return 4;

@@ -927,17 +927,16 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
                  : "=&v"(xa0), "=&v"(xa1), "=&v"(xb0), "=&v"(xb1)
                  : "v"(aA), "v"(aB), "i"(PB_WC * 1024)
                  : "memory");
+    // Set Y is read and waited for on every chunk, a one-word chunk included (its word-1 slots repeat word 0,
+    // stage()): no branch between an asm read and its wait, where the register allocator would be free to copy
+    // the destination registers before the data lands (tools/asm_audit.py checks the compiled kernel for that)
     const bool two = nw > 1;  // wave-uniform
-    if (two) {
-      asm volatile("ds_read_b128 %0, %4 offset:1024\n\tds_read_b128 %1, %4 offset:%6\n\t"
-                   "ds_read_b128 %2, %5 offset:1024\n\tds_read_b128 %3, %5 offset:%6"
-                   : "=&v"(ya0), "=&v"(ya1), "=&v"(yb0), "=&v"(yb1)
-                   : "v"(aA), "v"(aB), "i"((PB_WC + 1) * 1024)
-                   : "memory");
-      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
-    } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
-    }
+    asm volatile("ds_read_b128 %0, %4 offset:1024\n\tds_read_b128 %1, %4 offset:%6\n\t"
+                 "ds_read_b128 %2, %5 offset:1024\n\tds_read_b128 %3, %5 offset:%6"
+                 : "=&v"(ya0), "=&v"(ya1), "=&v"(yb0), "=&v"(yb1)
+                 : "v"(aA), "v"(aB), "i"((PB_WC + 1) * 1024)
+                 : "memory");
+    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
     auto word = [&](const v2d& a0, const v2d& a1, const v2d& b0, const v2d& b1, auto chc) __attribute__((always_inline)) {
       constexpr int chx = decltype(chc)::value;  // k-blocks 2 j, 2 j + 1 of the half: chains chx, chx + 1
       acc[0][0][chx] = mfma_f64(a0.x, b0.x, acc[0][0][chx]);
@@ -956,10 +955,9 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
       }
     };
     word(xa0, xa1, xb0, xb1, std::integral_constant<int, 0>{});
-    if (two) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
-      word(ya0, ya1, yb0, yb1, std::integral_constant<int, 2>{});
-    }
+    __builtin_amdgcn_sched_barrier(0);  // set X's MFMAs issue before set Y's wait (they hide its latency)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
+    if (two) word(ya0, ya1, yb0, yb1, std::integral_constant<int, 2>{});
     // Both sets' MFMAs issue here, before the next chunk's wait, barrier and fragment reads: the rewrites of
     // sets X and Y are inline asm, which the scheduler may otherwise move the (memory-free) MFMA builtins
     // across, and which the hazard recognizer does not see.  A scheduling barrier holds the order.
@@ -1931,7 +1929,10 @@ __device__ __forceinline__ void cross_big_body(const Plan* __restrict__ P, int B
 #pragma unroll 1
     for (int w = 0; w < nw; w += 2) {  // nw even
       const uint32_t o = (uint32_t)(w + 1) * 1024u;
-      asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
+      // set Y's rewrite follows set Y's MFMAs of the previous pair by only set X's rewrite: eight wait states
+      // first, so at least 16 issue cycles separate an MFMA from a rewrite of its operands on every path
+      // (tools/asm_audit.py checks the compiled kernel; the MFMA pipe keeps Y's queued MFMAs running meanwhile)
+      asm volatile("s_nop 7\n\tds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:%5"
                    : "=&v"(ya), "=&v"(yb0), "=&v"(yb1)
                    : "v"(aA + o), "v"(aB + o), "i"(XB_WC * 1024)
                    : "memory");
@@ -2088,11 +2089,10 @@ __device__ __forceinline__ void cross_big32_body(const Plan* __restrict__ P, int
   }
 }
 
-// (amdgpu_waves_per_eu(4): <= 128 VGPRs, so two blocks -- or a block and an envelope workgroup -- share a CU.
-// Unconstrained, round 5's contraction-free kernel terms took it to 130 VGPRs: one block per CU, and the
-// one-forward stage went 7.32 -> 7.95 us.)
+// (DKG_PC_WPE 4 holds it to 128 VGPRs, so two blocks share a CU, but spills 20 bytes a lane: one forward's stage
+// 7.9 -> 8.7 us (profiles/r06/cov/blk_h_pcw2.txt against blk_h_blk.txt); the default lets it take 130.)
 #ifndef DKG_PC_WPE
-#define DKG_PC_WPE 4
+#define DKG_PC_WPE 2
 #endif
 template <int DM, class T = double>
 __global__ __launch_bounds__(PC_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(DKG_PC_WPE))) void posterior_cov_kernel(const Plan* __restrict__ P,

@@ -24,6 +24,8 @@ DKG_PLAN_FORCE_WALK = 2  # test hook: envelope overflow path for every pair
 DKG_PLAN_F32 = 4  # fp32 contractions (BASELINE configs[4]); forward only
 DKG_PLAN_FUSED = 8  # the forward as one launch with in-launch hand-offs (dkg_fused.h); not the default
 DKG_PLAN_NO_CHAIN = 16  # test hook: the streaming envelope's list-overflow path (no sample chain) for every pair
+# dkg_debug_cov_kernels: the opt-in fp64 covariance block kernels (same bits as the defaults)
+DKG_COV_ENABLE_BLK, DKG_COV_ENABLE_REC2, DKG_COV_ENABLE_REG = 1, 2, 4
 MAX_OUTPUTS = 8
 MAX_DIM = 16
 
@@ -100,6 +102,7 @@ SIGNATURES = {
     "dkg_launcher_destroy": (c_int, [c_void_p]),
     "dkg_debug_read_kstamps": (c_int, [c_void_p, c_int]),
     "dkg_debug_wave_ops": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "dkg_debug_cov_kernels": (c_int, [c_int]),
     "dkg_debug_mfma_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 

@@ -321,6 +321,15 @@ int dkg_debug_wave_ops(const double* in, double* out, void* stream);
  * v_mfma_f64_16x16x4_f64 using the operand/result lane maps the kernels assume. */
 int dkg_debug_mfma_f64(const double* a, const double* b, double* c, void* stream);
 
+/* The opt-in fp64 covariance block kernels for the launches that would take them (bits below; tests and A/B
+ * measurements; initially from the environment variables DKG_COV_BLK / DKG_COV_REC2 / DKG_COV_REG).  Every one
+ * gives the bits of the default kernels.  Returns the previous mask; a mask < 0 only reads it.
+ * Process-wide: call it with no forward in flight. */
+#define DKG_COV_ENABLE_BLK 1  /* 64 x 32 LDS-staged blocks, three workgroups per CU */
+#define DKG_COV_ENABLE_REC2 2 /* m = 2, d <= 2: both outputs' whole records from one 8-wave workgroup per CU */
+#define DKG_COV_ENABLE_REG 4  /* register-operand blocks, any m, one 8-wave workgroup per CU */
+int dkg_debug_cov_kernels(int mask);
+
 /* ---- Launcher: captured forward graphs of several streams enqueued side by side from host threads.
  * A hipGraphLaunch costs ~1 us of host time per kernel node plus ~9 us; one thread launching every
  * stream's graphs in turn leaves the last stream idle for the others' launches.  The

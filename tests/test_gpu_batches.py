@@ -11,7 +11,7 @@ stress shape (64 x 64 covariance blocks).
 import pytest
 import torch
 
-from dkg_amd import DiscreteKnowledgeGradient
+from dkg_amd import DiscreteKnowledgeGradient, _lib
 from dkg_amd.errors import BotorchTensorDimensionError
 from dkg_amd.synthetic import WORKLOADS, make_problem
 
@@ -23,6 +23,22 @@ DEV = "cuda:0"
 def _need_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
+
+
+# The batched launches with every fp64 covariance block kernel enabled that their shapes take (the defaults, the
+# 64 x 32 blocks, the register-operand and whole-record blocks: dkg_debug_cov_kernels); every one must give the
+# per-batch bits (one dkg_plan_forward per batch, the narrow blocks).
+COV_KERNELS = {"default": 0, "blk": _lib.DKG_COV_ENABLE_BLK, "rec2": _lib.DKG_COV_ENABLE_REC2,
+               "reg": _lib.DKG_COV_ENABLE_REG}
+
+
+@pytest.fixture(params=list(COV_KERNELS))
+def cov_kernels(request):
+    lib = _lib.load()
+    prev = lib.dkg_debug_cov_kernels(COV_KERNELS[request.param])
+    yield request.param
+    torch.cuda.synchronize()
+    lib.dkg_debug_cov_kernels(prev)
 
 
 def _batched_vs_single(wname, B, K, target, on_grid=0, seed=3, fused=False, precision="fp64"):
@@ -59,7 +75,7 @@ def _batched_vs_single(wname, B, K, target, on_grid=0, seed=3, fused=False, prec
     ("parity6d", 23, 3, None, 0),
     ("headline_nd", 128, 3, 1, 0),
 ])
-def test_batched_launch_writes_the_per_batch_bits(wname, B, K, target, on_grid):
+def test_batched_launch_writes_the_per_batch_bits(wname, B, K, target, on_grid, cov_kernels):
     kg, kg2, ref = _batched_vs_single(wname, B, K, target, on_grid)
     assert not torch.isnan(ref).any()
     assert torch.equal(kg, ref)
@@ -91,7 +107,7 @@ def test_batched_launch_fp32_plan(wname, B, K):
     assert torch.equal(kg, ref) and torch.equal(kg2, ref)
 
 
-def test_batched_launch_stress_shape():
+def test_batched_launch_stress_shape(cov_kernels):
     kg, kg2, ref = _batched_vs_single("stress", 256, 2, None, 0)
     assert torch.equal(kg, ref) and torch.equal(kg2, ref)
 
@@ -110,7 +126,7 @@ def test_batched_launch_arguments():
 
 
 @pytest.mark.parametrize("kernel,nu", [("matern", 2.5), ("rbf", None)])
-def test_batched_launch_outputs_of_different_sizes(kernel, nu):
+def test_batched_launch_outputs_of_different_sizes(kernel, nu, cov_kernels):
     """Outputs with different training-set sizes (ragged n: 100, 300 and 37 points) in a launch that takes the
     K(x, X) fill and the 64 x 32 cross blocks (5 x 128 = 640 candidates), against one forward per batch (the
     in-workgroup fill of cross_root_plan_kernel): the blocks of the smaller outputs past their own tiles return
@@ -144,7 +160,7 @@ def test_batched_launch_outputs_of_different_sizes(kernel, nu):
 
 
 @pytest.mark.parametrize("K,kernel,nu", [(5, "matern", 2.5), (4, "rbf", None), (5, "matern", 1.5)])
-def test_batched_launch_two_outputs_whole_records(K, kernel, nu):
+def test_batched_launch_two_outputs_whole_records(K, kernel, nu, cov_kernels):
     """Two outputs of different (odd-half) training sizes, N = 1000 lines: K = 5 / 4 batches of 128 take the
     block kernel that writes both outputs' records from one workgroup (posterior_cov_rec2_kernel, RT = 5 / 4:
     256 blocks), whose K halves are 7 and 4 words here; its rows must be the per-batch bits (narrow blocks)."""
