@@ -58,7 +58,7 @@ FP64_VALU_MEASURED_TFLOPS = 61.4
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 SIMDS, CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMDs
-PMC_DIR = os.path.join(REPO, "profiles", "r05")
+PMC_DIR = os.path.join(REPO, "profiles", "r06")
 
 
 def parse():

@@ -18,22 +18,30 @@ import json
 import sys
 
 KERNELS = {"cross_root_plan_kernel": "cross_root_kernel", "cross_kfill_kernel": "cross_kfill_kernel",
-           "cross_big_kernel": "cross_big_kernel",
+           "cross_big_kernel": "cross_big_kernel", "cross_big32_kernel": "cross_big32_kernel",
+           "posterior_cov_big32_kernel": "posterior_cov_big32_kernel",
+           "posterior_cov_blk_kernel": "posterior_cov_blk_kernel", "posterior_cov_reg_kernel": "posterior_cov_reg_kernel",
+           "posterior_cov_rec2_kernel": "posterior_cov_rec2_kernel",
            "posterior_cov_kernel": "posterior_cov_kernel", "posterior_cov_wide_kernel": "posterior_cov_wide_kernel",
            "posterior_cov_big_kernel": "posterior_cov_big_kernel", "envelope_kernel": "envelope_kernel"}
 # bench.py's stages: the kernels one launch of the timed region runs per stage (large n or many candidates:
 # the K(x, X) fill before the cross kernel; large B x N: the 64 x 64 or LDS-staged 64 x 128 covariance
 # blocks), summed per launch
-STAGES = {"cross_root_kernel": ("cross_root_kernel", "cross_kfill_kernel", "cross_big_kernel"),
-          "posterior_cov_kernel": ("posterior_cov_kernel", "posterior_cov_wide_kernel", "posterior_cov_big_kernel"),
+STAGES = {"cross_root_kernel": ("cross_root_kernel", "cross_kfill_kernel", "cross_big_kernel", "cross_big32_kernel"),
+          "posterior_cov_kernel": ("posterior_cov_kernel", "posterior_cov_wide_kernel", "posterior_cov_big_kernel",
+                                   "posterior_cov_big32_kernel", "posterior_cov_blk_kernel", "posterior_cov_reg_kernel",
+                                   "posterior_cov_rec2_kernel"),
           "envelope_kernel": ("envelope_kernel",)}
 # A stage launches one of its alternatives (the K(x, X) fill goes with either cross kernel); the bench's
 # diagnostics also run single-batch forwards, so the timed region's alternative is the one for the largest
 # launches: the last listed whose main kernel was dispatched (the big blocks are chosen only for launches with
 # at least one block per CU, and fp32 plans never take them).
-ALTERNATIVES = {"cross_root_kernel": (("cross_root_kernel", "cross_kfill_kernel"), ("cross_big_kernel", "cross_kfill_kernel")),
+ALTERNATIVES = {"cross_root_kernel": (("cross_root_kernel", "cross_kfill_kernel"), ("cross_big_kernel", "cross_kfill_kernel"),
+                                      ("cross_big32_kernel", "cross_kfill_kernel")),
                 "posterior_cov_kernel": (("posterior_cov_kernel",), ("posterior_cov_wide_kernel",),
-                                         ("posterior_cov_big_kernel",)),
+                                         ("posterior_cov_big_kernel",), ("posterior_cov_big32_kernel",),
+                                         ("posterior_cov_blk_kernel",), ("posterior_cov_reg_kernel",),
+                                         ("posterior_cov_rec2_kernel",)),
                 "envelope_kernel": (("envelope_kernel",),)}
 
 
