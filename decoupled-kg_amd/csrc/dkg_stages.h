@@ -743,10 +743,10 @@ __device__ __forceinline__ double2 gload_d2(const double* p) {
 // are in flight, so the epilogue only stores (in registers they would stay live across the contraction).
 // Returns the r^2 == 0 bits (Plan::dup), one per element.  scaled_r2_dm's and kernel_term_nc's arithmetic
 // (compiled without FP contraction, dkg_common.h), so the terms are posterior_cov_body's bits.
-template <int DM, class T>
+template <int DM, class T, class Sink>
 __device__ __forceinline__ uint32_t big_block_terms(const Plan* __restrict__ P, const dkg_output& o,
                                                     const double* __restrict__ xnew, int B, int tr, int tc, int lane,
-                                                    double* __restrict__ kvs) {
+                                                    Sink&& sink) {
   const int N = P->N, d = P->d;
   const double os = o.outputscale;
   const int kind = o.kernel;
@@ -785,7 +785,7 @@ __device__ __forceinline__ uint32_t big_block_terms(const Plan* __restrict__ P, 
           }
           const double kv = os * kernel_term_nc<KIND>(r2, tab);  // rounded (stored), as posterior_cov_body
           const int e = (g * 2 + h) * 4 + r;
-          kvs[e * 64 + lane] = kv;
+          sink(e, kv);
           zero_r2 |= (r2 == 0.0 ? 1u : 0u) << e;
         }
       }
@@ -799,17 +799,30 @@ __device__ __forceinline__ uint32_t big_block_terms(const Plan* __restrict__ P, 
   return zero_r2;
 }
 
+template <int DM, class T>
+__device__ __forceinline__ uint32_t big_block_terms(const Plan* __restrict__ P, const dkg_output& o,
+                                                    const double* __restrict__ xnew, int B, int tr, int tc, int lane,
+                                                    double* __restrict__ kvs) {
+  return big_block_terms<DM, T>(P, o, xnew, B, tr, tc, lane,
+                                [&](int e, double kv) __attribute__((always_inline)) { kvs[e * 64 + lane] = kv; });
+}
+
 constexpr int PB_WAVES = 4;
 constexpr int PB_RT = 4;  // candidate tiles per block
 constexpr int PB_CT = 4;  // line tiles per block
 constexpr int PB_WC = 2;  // words (two k-blocks each) per staged chunk; even, so chains restart in step
+// the kernel terms in registers (16 per lane) instead of parked in LDS: the LDS then holds the stage buffers only
+#ifndef DKG_PB_KVREG
+#define DKG_PB_KVREG 0
+#endif
+constexpr bool PB_KVREG = DKG_PB_KVREG != 0;
 constexpr int PB_STAGE = (PB_RT + PB_CT) * PB_WC * 64;  // 16-byte words per stage buffer
 #ifndef DKG_PB_NSTG
 #define DKG_PB_NSTG 2
 #endif
 constexpr int PB_NSTG = DKG_PB_NSTG;                               // stage buffers: chunks in flight + the one computed
 // the stage buffers, then the kernel terms (16 per lane per wave): 64 KiB, two workgroups per CU
-constexpr size_t PB_LDS = PB_NSTG * (size_t)PB_STAGE * 16 + (size_t)PB_WAVES * 16 * 64 * 8;
+constexpr size_t PB_LDS = PB_NSTG * (size_t)PB_STAGE * 16 + (PB_KVREG ? 0 : (size_t)PB_WAVES * 16 * 64 * 8);
 
 template <int DM>
 __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(2))) void posterior_cov_big_kernel(
@@ -881,7 +894,17 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   // r^2 == 0 (Plan::dup) as one bit per element.
   const double os = o.outputscale;
   double* kvs = reinterpret_cast<double*>(stg + (size_t)PB_NSTG * PB_STAGE) + (size_t)wave * 16 * 64;
-  const uint32_t zero_r2 = big_block_terms<DM, double>(P, o, xnew, B, ti0 + 2 * rp, tk0 + 2 * cp, lane, kvs);
+  double kvr[PB_KVREG ? 16 : 1];
+  uint32_t zero_r2;
+  if constexpr (PB_KVREG) {
+    zero_r2 = big_block_terms<DM, double>(P, o, xnew, B, ti0 + 2 * rp, tk0 + 2 * cp, lane,
+                                          [&](int e, double kv) __attribute__((always_inline)) {
+                                            asm volatile("" : "+v"(kv));  // rounded here (never fused later)
+                                            kvr[e] = kv;
+                                          });
+  } else {
+    zero_r2 = big_block_terms<DM, double>(P, o, xnew, B, ti0 + 2 * rp, tk0 + 2 * cp, lane, kvs);
+  }
   KST(st, 2);
   for (int c = 0; c < nc; ++c) {
     // chunk c landed (this wave's pieces), then every wave's: the later chunks' DMAs stay in flight
@@ -990,7 +1013,8 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
         const int b = 16 * (ti0 + 2 * rp + h) + mfma_drow<double>(le, r);
         const int e = (g * 2 + h) * 4 + r;
         if (b < B && k < N) {
-          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] = kvs[e * 64 + le] - tot[h][g][r];
+          P->cov_all[(size_t)b * P->cov_stride + (size_t)k * rec + oi] =
+              (PB_KVREG ? kvr[PB_KVREG ? e : 0] : kvs[e * 64 + le]) - tot[h][g][r];
           if (DKG_DUP_MARK && ((zero_r2 >> e) & 1)) atomicMin(&P->dup[b], k);  // Plan::dup
         }
       }

@@ -202,21 +202,27 @@ class _HostForwardFn(torch.autograd.Function):
     def forward(ctx, X, acq):
         d = X.shape[-1]
         batch = X.shape[:-2]
-        flat = X.detach().reshape(-1, d)
-        if flat.dtype != torch.double:
-            flat = flat.to(torch.double)
+        xs = X.detach()
+        if xs.dtype != torch.double or not xs.is_contiguous():
+            xs = xs.to(torch.double).contiguous()
+        B = xs.numel() // d
         if ctx.needs_input_grad[0]:
-            kg, dkg = acq._plan_for(flat.shape[0], grad=True).forward_grad_host(flat)
+            plan = acq._plan_grad
+            if plan is None or plan.max_B < B:
+                plan = acq._plan_for(B, grad=True)
+            kg, dkg = plan.forward_grad_host_shaped(xs, B, batch, X.shape)
             ctx.save_for_backward(dkg)
-            ctx.xshape, ctx.xdtype = X.shape, X.dtype
-        else:
-            kg = acq._plan_for(flat.shape[0]).forward_host(flat.contiguous())
+            ctx.xdtype = X.dtype
+            return kg if X.dtype == torch.double else kg.to(X.dtype)
+        kg = acq._plan_for(B).forward_host(xs.reshape(B, d))
         return kg.to(X.dtype).reshape(batch)
 
     @staticmethod
     def backward(ctx, grad):
-        (dkg,) = ctx.saved_tensors
-        return (grad.reshape(-1, 1).to(dkg) * dkg).reshape(ctx.xshape).to(ctx.xdtype), None
+        (dkg,) = ctx.saved_tensors  # shaped as X: [*batch, 1, d]
+        g = grad.to(dkg) if grad.dtype != dkg.dtype else grad
+        out = g.reshape(g.shape + (1, 1)) * dkg
+        return (out if ctx.xdtype == torch.double else out.to(ctx.xdtype)), None
 
 
 class DiscreteKnowledgeGradient(_Base):
@@ -368,12 +374,15 @@ class DiscreteKnowledgeGradient(_Base):
         if X.dim() > 2 and X.shape[-2] != 1:
             raise ValueError(f"Expected X to be `batch_shape x q=1 x d`, but got X with shape {tuple(X.shape)}.")
         self._refresh()
-        flat = X.detach().reshape(-1, d)
-        if flat.dtype != torch.double or flat.device.type != "cpu":
-            flat = flat.to("cpu", torch.double)
-        kg, dkg = self._plan_for(flat.shape[0], grad=True).forward_grad_host(flat)
+        xs = X.detach()
+        if xs.dtype != torch.double or xs.device.type != "cpu" or not xs.is_contiguous():
+            xs = xs.to("cpu", torch.double).contiguous()
+        B = xs.numel() // d
+        plan = self._plan_grad
+        if plan is None or plan.max_B < B:
+            plan = self._plan_for(B, grad=True)
         batch = X.shape[:-2] if X.dim() > 2 else X.shape[:-1]
-        return kg.reshape(batch), dkg.reshape(X.shape)
+        return plan.forward_grad_host_shaped(xs, B, batch, X.shape)
 
     def forward_pairs(self, X: Tensor) -> Tensor:
         """KG per (candidate, scalarisation): [B, S] (the per-``j`` values of ``:200-233``)."""

@@ -323,9 +323,26 @@ class ForwardPlan:
                 return self._forward_grad_hostx(X_host, B, d)
             return self._forward_grad_host(X_host, B, d, graph)
 
+    def forward_grad_host_shaped(self, X_host: torch.Tensor, B: int, kshape, xshape):
+        """``forward_grad_host`` for a contiguous fp64 host tensor holding B candidates in any shape (e.g. the
+        ``[*batch, 1, d]`` X of ``optimize_acqf``), the results viewed as ``kshape`` / ``xshape``: the
+        B = 1 L-BFGS-B path, with no reshape of X and one copy plus two views out (each torch op is about a
+        microsecond of host time on a call whose device chain is ~30 us)."""
+        d = self.state.d
+        if (self.grad and 0 < B <= self.max_B and B * d <= _lib.DKG_XARG_MAX
+                and torch.cuda.current_device() == self.device.index):
+            r = self._forward_grad_hostx_raw(X_host, B, d)
+            return r[:B].view(kshape), r[B:].view(xshape)
+        kg, dkg = self.forward_grad_host(X_host.reshape(B, d))
+        return kg.reshape(kshape), dkg.reshape(xshape)
+
     def _forward_grad_hostx(self, X_host: torch.Tensor, B: int, d: int):
+        r = self._forward_grad_hostx_raw(X_host, B, d)
+        return r[:B], r[B:].view(B, d)
+
+    def _forward_grad_hostx_raw(self, X_host: torch.Tensor, B: int, d: int):
         # the plan's device is current; one C call launches, lets the envelope kernel write the pinned
-        # buffer and synchronises the stream
+        # buffer and synchronises the stream; returns a copy of [KG | dKG/dx]
         io = self._io.get(B) if getattr(self, "_io", None) is not None else None
         if io is None:
             self._host_buffers(d)
@@ -340,8 +357,7 @@ class ForwardPlan:
                                   _raw_stream(self.device))
         if st:
             _lib.check(st, "dkg_plan_forward_grad_hostx")
-        r = out.clone()
-        return r[:B], r[B:].view(B, d)
+        return out.clone()
 
     def _host_buffers(self, d: int):
         """The pinned host and device staging buffers of the host entries (made once, sized for max_B)."""

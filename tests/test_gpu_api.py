@@ -171,6 +171,27 @@ def test_value_and_grad_host_matches_forward_and_autograd(B, graph):
         assert torch.equal(kg2, kg) and torch.equal(g2.squeeze(-2), g)
 
 
+def test_value_and_grad_host_input_forms():
+    """value_and_grad_host takes X as [B, d], [*batch, 1, d], fp32 or a non-contiguous view: results shaped
+    like the batch and like X, the bits of the contiguous fp64 call."""
+    model, D, X, W = make_problem(WORKLOADS["small"])
+    acq = DiscreteKnowledgeGradient(model, D, W)
+    Xb = X[:6].clone()
+    kg, g = acq.value_and_grad_host(Xb.reshape(3, 2, 1, 2))
+    assert kg.shape == (3, 2) and g.shape == (3, 2, 1, 2)
+    kg2, g2 = acq.value_and_grad_host(Xb)
+    assert kg2.shape == (6,) and g2.shape == (6, 2)
+    assert torch.equal(kg.reshape(-1), kg2) and torch.equal(g.reshape(6, 2), g2)
+    wide = torch.zeros(6, 4, dtype=torch.double)
+    wide[:, ::2] = Xb
+    kg3, g3 = acq.value_and_grad_host(wide[:, ::2])  # non-contiguous
+    assert torch.equal(kg3, kg2) and torch.equal(g3, g2)
+    X32 = Xb.float()
+    kg4, g4 = acq.value_and_grad_host(X32.unsqueeze(-2))
+    kg5, g5 = acq.value_and_grad_host(X32.double().unsqueeze(-2))
+    assert torch.equal(kg4, kg5) and torch.equal(g4, g5)
+
+
 def test_value_and_grad_host_follows_a_refit_model():
     model, D, X, W = make_problem(WORKLOADS["small"])
     acq = DiscreteKnowledgeGradient(model, D, W)
