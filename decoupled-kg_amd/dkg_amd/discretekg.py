@@ -202,9 +202,9 @@ class _HostForwardFn(torch.autograd.Function):
     def forward(ctx, X, acq):
         d = X.shape[-1]
         batch = X.shape[:-2]
-        xs = X.detach()
-        if xs.dtype != torch.double or not xs.is_contiguous():
-            xs = xs.to(torch.double).contiguous()
+        xs = X  # (inside an autograd.Function's forward: its data pointer is read)
+        if xs.dtype is not torch.double or not xs.is_contiguous():
+            xs = xs.detach().to(torch.double).contiguous()
         B = xs.numel() // d
         if ctx.needs_input_grad[0]:
             plan = acq._plan_grad
@@ -374,9 +374,9 @@ class DiscreteKnowledgeGradient(_Base):
         if X.dim() > 2 and X.shape[-2] != 1:
             raise ValueError(f"Expected X to be `batch_shape x q=1 x d`, but got X with shape {tuple(X.shape)}.")
         self._refresh()
-        xs = X.detach()
-        if xs.dtype != torch.double or xs.device.type != "cpu" or not xs.is_contiguous():
-            xs = xs.to("cpu", torch.double).contiguous()
+        xs = X  # (its data pointer is read, nothing is recorded for autograd)
+        if xs.dtype is not torch.double or not xs.is_cpu or not xs.is_contiguous():
+            xs = xs.detach().to("cpu", torch.double).contiguous()
         B = xs.numel() // d
         plan = self._plan_grad
         if plan is None or plan.max_B < B:

@@ -326,38 +326,38 @@ class ForwardPlan:
     def forward_grad_host_shaped(self, X_host: torch.Tensor, B: int, kshape, xshape):
         """``forward_grad_host`` for a contiguous fp64 host tensor holding B candidates in any shape (e.g. the
         ``[*batch, 1, d]`` X of ``optimize_acqf``), the results viewed as ``kshape`` / ``xshape``: the
-        B = 1 L-BFGS-B path, with no reshape of X and one copy plus two views out (each torch op is about a
-        microsecond of host time on a call whose device chain is ~30 us)."""
+        B = 1 L-BFGS-B path, with no reshape of X and the results copied out once through numpy (a torch
+        slice or view costs about a microsecond of host time each, on a call whose device chain is ~30 us)."""
         d = self.state.d
         if (self.grad and 0 < B <= self.max_B and B * d <= _lib.DKG_XARG_MAX
                 and torch.cuda.current_device() == self.device.index):
             r = self._forward_grad_hostx_raw(X_host, B, d)
-            return r[:B].view(kshape), r[B:].view(xshape)
+            return torch.from_numpy(r[:B].reshape(kshape)), torch.from_numpy(r[B:].reshape(xshape))
         kg, dkg = self.forward_grad_host(X_host.reshape(B, d))
         return kg.reshape(kshape), dkg.reshape(xshape)
 
     def _forward_grad_hostx(self, X_host: torch.Tensor, B: int, d: int):
         r = self._forward_grad_hostx_raw(X_host, B, d)
-        return r[:B], r[B:].view(B, d)
+        return torch.from_numpy(r[:B]), torch.from_numpy(r[B:].reshape(B, d))
 
     def _forward_grad_hostx_raw(self, X_host: torch.Tensor, B: int, d: int):
         # the plan's device is current; one C call launches, lets the envelope kernel write the pinned
-        # buffer and synchronises the stream; returns a copy of [KG | dKG/dx]
+        # buffer and synchronises the stream; returns a numpy copy of [KG | dKG/dx]
         io = self._io.get(B) if getattr(self, "_io", None) is not None else None
         if io is None:
             self._host_buffers(d)
             dx = self._dx[:B * d]
+            out = self._hout[:B * (d + 1)]
             io = self._io[B] = (dx.data_ptr(), self._dout[:B].data_ptr(), self._dout[B:B * (d + 1)].data_ptr(),
-                                self._hout[:B * (d + 1)])
+                                out.data_ptr(), out.numpy())
         xc = X_host
         if xc.dtype != torch.double or not xc.is_contiguous():
             xc = xc.to(torch.double).contiguous()
-        out = io[3]
-        st = self._fwd_grad_hostx(self.host, self._dev_ptr, xc.data_ptr(), io[0], B, io[1], io[2], out.data_ptr(),
+        st = self._fwd_grad_hostx(self.host, self._dev_ptr, xc.data_ptr(), io[0], B, io[1], io[2], io[3],
                                   _raw_stream(self.device))
         if st:
             _lib.check(st, "dkg_plan_forward_grad_hostx")
-        return out.clone()
+        return io[4].copy()
 
     def _host_buffers(self, d: int):
         """The pinned host and device staging buffers of the host entries (made once, sized for max_B)."""
