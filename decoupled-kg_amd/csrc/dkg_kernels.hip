@@ -605,7 +605,7 @@ int set_cov_enabled(int mask) {
 
 // Off unless enabled: alone a 5-batch headline launch takes 27.7 us against the 64 x 64 blocks' 31.4, but
 // with the four launch streams of bench.py the 64 x 64 blocks give the higher rate (10.0-10.4 against
-// 9.5-9.7 M KG-evals/s at --steps 20, profiles/r06/cov/covab_*.txt): with forwards in flight the rate is the
+// 9.5-9.7 M KG-evals/s at --steps 20, profiles/r06/bench/covab.txt): with forwards in flight the rate is the
 // stages' summed CU time, not one launch's latency.  (m >= 3 alone: 164 against 143.7 us at configs[4].)
 static bool cov_blk(int N, int B, int m) {
   return (cov_enabled() & DKG_COV_ENABLE_BLK) && N >= 64 &&
@@ -631,7 +631,7 @@ static int cov_reg_rt(int N, int B, int m) {
 // Off unless DKG_COV_REC2=1 (or 4 / 5 to force RT): the fastest covariance launch alone (a 5-batch headline launch
 // 23.0 us, 0.38 of the fp64 roof, against 31.4), but one 8-wave workgroup of 256 VGPRs and 121 KB of LDS takes a
 // CU whole, so nothing of the other streams' forwards runs beside it: 8.9-9.1 against 10.0-10.4 M KG-evals/s in
-// bench.py's --steps 20 line (profiles/r06/cov/covab_*.txt).
+// bench.py's --steps 20 line (profiles/r06/bench/covab.txt).
 static int cov_rec2_rt(int N, int B) {
   if (!(cov_enabled() & DKG_COV_ENABLE_REC2) || N < 32) return 0;
   auto blocks = [&](int rt) { return (size_t)((N + 31) / 32) * ((B + 16 * rt - 1) / (16 * rt)); };
