@@ -755,11 +755,6 @@ int dkg_debug_cov_kernels(int mask) {
   return set_cov_enabled(mask);
 }
 
-int dkg_debug_env_items(int n) {
-  if (n < 0) return env_items_per_wg();
-  return set_env_items(n);
-}
-
 int dkg_debug_wave_ops(const double* in, double* out, void* stream) {
   if (!in || !out) return fail(DKG_ERR_ARG, "NULL pointer");
   return hip_check(launch_debug_wave(in, out, (hipStream_t)stream), "debug_wave_kernel");

@@ -1468,18 +1468,6 @@ __device__ __forceinline__ void dma_to_lds(const double* __restrict__ src, doubl
   }
 }
 
-// dma_to_lds through glds16 (dkg_common.h): the compiler does not see these copies, so it inserts no wait for
-// them before later LDS reads -- the caller waits (vmcnt; a __syncthreads() also drains them).  The multi-candidate
-// envelope prefetches the next candidate's records this way while the current candidate's pairs run.
-__device__ __forceinline__ void dma_to_lds_hidden(const double* __restrict__ src, double* dst, int n, int wave,
-                                                  int nwaves, int lane) {
-  const int chunks = (n + 1) / 2;  // 16-byte pieces
-  for (int c0 = wave * 64; c0 < chunks; c0 += nwaves * 64) {
-    const int c = min(c0 + lane, chunks - 1);
-    glds16(src + 2 * c, (uint32_t)reinterpret_cast<uintptr_t>(dst + 2 * c0));
-  }
-}
-
 // Waves per SIMD the register allocation targets.  The forward up to 17
 // slots fits 4 (<= 128 VGPRs: two envelope workgroups, or an envelope and a
 // covariance workgroup, share a CU) without a spill: one pair per wave
@@ -1517,8 +1505,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
                                               const double* __restrict__ mux_all, const double* __restrict__ wts,
                                               const int* __restrict__ dupv, long long cov_stride, int bpad, int b,
                                               int g, int G, double* smem, unsigned long long* st,
-                                              const Handoff* ho = nullptr, double* __restrict__ hout = nullptr,
-                                              int ipw = 1, int item = 0, int b_next = -1) {
+                                              const Handoff* ho = nullptr, double* __restrict__ hout = nullptr) {
   static_assert(!HO || (!GRAD && !STREAM), "the fused forward stages its lines (no gradient, no streaming)");
   // per output i: y_std, y_mean, noise, outputscale, noiseless variance at x_b, mean at x_b (model space),
   // and line 0's inputs: the mean and slope component it is built from (x_b's own, or, when x_b coincides
@@ -1557,15 +1544,9 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   // (the staged forward without mu_D records: its covariance records start where they would)
   constexpr bool ICP = DKG_ICP && !GRAD && !STREAM && !HO;  // intercepts from the plan's cache (Plan::icpt)
   constexpr bool MU_STAGED = !ICP;
-  // Multi-candidate workgroups (staged forward, ipw > 1: envelope_kernel runs `ipw` candidates in turn): mu_D's
-  // records are staged once, the covariance records in two buffers -- item i's in buffer i & 1, the next
-  // candidate's DMA'd into the other one while item i's pairs run (b_next).
-  constexpr bool MULTI_OK = !GRAD && !STREAM && !HO && !ICP;
-  const int nbuf = (MULTI_OK && ipw > 1) ? 2 : 1;
   double* lmu = smem + STAGE_FRONT;
-  double* lcv0 = lmu + ((STREAM || MU_STAGED) ? SLp : 0);
-  double* lcv = lcv0 + (size_t)(nbuf == 2 ? (item & 1) : 0) * SLp;
-  double* lw = lcv0 + (size_t)nbuf * SLp;
+  double* lcv = lmu + ((STREAM || MU_STAGED) ? SLp : 0);
+  double* lw = lcv + SLp;
   double* skg = lw + ((S * m + 1) & ~1);  // KG_j of the group's pairs (summed in j order)
   double* sbuf = skg + ((S + 1) & ~1);
   // GRAD regions: per-wave index lists, per-wave Q_D accumulators u_i[c], the
@@ -1618,11 +1599,8 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   const double* wsrc = wts;
   if constexpr (!STREAM) {
     // (the staged forward reads its intercepts from the plan's cache instead: no mu_D records in LDS)
-    // (a multi-candidate workgroup's later items: mu_D is staged, their records were prefetched)
-    if (item == 0) {
-      if constexpr (MU_STAGED) dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
-      if constexpr (!HO) dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
-    }
+    if constexpr (MU_STAGED) dma_to_lds(mu_src[0], lmu, N * MP, wave, SW, lane_k);
+    if constexpr (!HO) dma_to_lds(cv_src[0], lcv, N * MP, wave, SW, lane_k);
   }
   if constexpr (GRAD) {
     // the candidate's q_i and J_i rows (row-major in the workspace) by LDS-DMA with the line data, so
@@ -1698,14 +1676,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
       lcv[e] = __builtin_nan("");
     }
   };
-  if constexpr (!STREAM) {
-    if (item == 0) {
-      pad_lines(max(N * MP, SLd), pad_end);
-      if (nbuf == 2)  // the second record buffer's padding (never overwritten: its DMAs end at SLd)
-        for (int e = max(N * MP, SLd) + (int)threadIdx.x; e < pad_end; e += blockDim.x)
-          lcv0[SLp + e] = __builtin_nan("");
-    }
-  }
+  if constexpr (!STREAM) pad_lines(max(N * MP, SLd), pad_end);
   // pairs j0 .. j1-1 of the candidate, one per wave (gridDim.y = ceil(S / SW), envelope_geometry)
   const int j0 = g * SW, j1 = min(S, j0 + SW);
   // Staged forward with the plan's intercept cache (Plan::icpt): this wave's intercepts a_k (slot t of lane
@@ -2044,14 +2015,6 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
 #undef STG_W0
 #undef STG_W1
 
-  // multi-candidate workgroup: the next candidate's records into the other buffer (every wave is done with it:
-  // it held the previous item, which ended in a __syncthreads()); waited for at this item's closing
-  // __syncthreads(), whose release fence drains the DMAs, and again by the next item's own wait
-  if constexpr (MULTI_OK) {
-    if (nbuf == 2 && b_next >= 0)
-      dma_to_lds_hidden(cov_all + (size_t)b_next * cov_stride, lcv0 + (size_t)((item + 1) & 1) * SLp, N * MP, wave,
-                        SW, lane_k);
-  }
   if (const int j = j0 + wave; j < j1) {
     const int lane = lane_k;
     // ---- line coefficients (wave uniform; shared with lines_export_kernel)
@@ -2675,7 +2638,7 @@ __device__ __forceinline__ void envelope_body(const Plan* __restrict__ P, int B,
   KST_END(st);
 }
 
-template <int MAXL, int M, bool GRAD, bool STREAM, bool MULTI = false>
+template <int MAXL, int M, bool GRAD, bool STREAM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_per_eu(MAXL, M, GRAD, STREAM)))) void envelope_kernel(const Plan* __restrict__ P, int B, double* __restrict__ kg,
                                                        double* __restrict__ pairs_out, int dst,
                                                        const double* __restrict__ xnew, double* __restrict__ dkg,
@@ -2685,26 +2648,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(env_waves_p
                                                        const double* __restrict__ mux_all,
                                                        const double* __restrict__ wts,
                                                        const int* __restrict__ dupv, long long cov_stride,
-                                                       int bpad, double* __restrict__ hout, int split, int ipw) {
+                                                       int bpad, double* __restrict__ hout, int split) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (DKG_ABLATIONS && (__builtin_amdgcn_readfirstlane(P->debug_env) & 2)) return;  // ablation: empty envelope stage
   // 1-D grid: the `split` workgroups of one candidate side by side on one XCD (xcd_group), so its line
-  // records come from HBM once and from that XCD's L2 for the others.  ipw > 1 (staged forward only,
-  // env_items_per_wg): workgroup (blk, g) runs candidates blk ipw .. blk ipw + ipw - 1 in turn.
-  if constexpr (!MULTI || GRAD || STREAM) {
-    int b, g;
-    if (!xcd_group(blockIdx.x, B, split, b, g)) return;
-    envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
-                                         dupv, cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout);
-  } else {
-    int blk, g;
-    if (!xcd_group(blockIdx.x, (B + ipw - 1) / ipw, split, blk, g)) return;
-    const int b0 = blk * ipw, nb = min(ipw, B - b0);
-    for (int i = 0; i < nb; ++i)
-      envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all,
-                                           wts, dupv, cov_stride, bpad, b0 + i, g, split, smem, kst_slot(dst, P, 2),
-                                           nullptr, hout, ipw, i, i + 1 < nb ? b0 + i + 1 : -1);
-  }
+  // records come from HBM once and from that XCD's L2 for the others
+  int b, g;
+  if (!xcd_group(blockIdx.x, B, split, b, g)) return;
+  envelope_body<MAXL, M, GRAD, STREAM>(P, B, kg, pairs_out, dst, xnew, dkg, mu_all, cov_all, var_all, mux_all, wts,
+                                       dupv, cov_stride, bpad, b, g, split, smem, kst_slot(dst, P, 2), nullptr, hout);
 }
 
 // The lines of every (candidate, scalarisation) pair of the plan's last
@@ -2775,33 +2727,15 @@ struct EnvLaunch {
   const double* xnew;  // GRAD
   double* dkg;         // GRAD
   double* hout;        // GRAD: pinned host [kg | dkg] (dkg_plan_forward_grad_hostx), nullable
-  int ipw;             // staged forward: candidates per workgroup (env_items_per_wg); the grid and LDS follow it
 };
 
 template <int MAXL, int M, bool GRAD, bool STREAM>
 hipError_t launch_env_t(const EnvLaunch& a) {
+  raise_lds_limit((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>, a.lds);
   const Plan& h = *a.host;
-  // multi-candidate workgroups: the staged forward only (envelope_body MULTI_OK), one more record buffer
-  const int ipw = (!GRAD && !STREAM && !DKG_ICP && a.ipw > 1) ? a.ipw : 1;
-  dim3 grid = a.grid;
-  size_t lds = a.lds;
-  if (ipw > 1) {
-    grid = dim3(xcd_group_size((a.B + ipw - 1) / ipw, h.split));
-    lds += (size_t)stage_stride(h.N, cov_rec(M)) * sizeof(double);
-  }
-  if constexpr (!GRAD && !STREAM && !DKG_ICP) {
-    if (ipw > 1) {
-      raise_lds_limit((const void*)envelope_kernel<MAXL, M, GRAD, STREAM, true>, lds);
-      hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM, true>), grid, a.block, lds, a.s, a.dev, a.B, a.kg,
-                         a.pairs, a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights, h.dup,
-                         (long long)h.cov_stride, h.bpad, a.hout, h.split, ipw);
-      return hipGetLastError();
-    }
-  }
-  raise_lds_limit((const void*)envelope_kernel<MAXL, M, GRAD, STREAM>, lds);
-  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), grid, a.block, lds, a.s, a.dev, a.B, a.kg, a.pairs,
+  hipLaunchKernelGGL((envelope_kernel<MAXL, M, GRAD, STREAM>), a.grid, a.block, a.lds, a.s, a.dev, a.B, a.kg, a.pairs,
                      a.dst, a.xnew, a.dkg, h.mu_all, h.cov_all, h.var_all, h.mux_all, h.weights, h.dup,
-                     (long long)h.cov_stride, h.bpad, a.hout, h.split, 1);
+                     (long long)h.cov_stride, h.bpad, a.hout, h.split);
   return hipGetLastError();
 }
 

@@ -187,8 +187,6 @@ constexpr int KST_WG = 1024;
 hipError_t launch_debug_wave(const double* in, double* out, hipStream_t s);
 // The opt-in fp64 covariance block kernels (dkg_debug_cov_kernels): sets the mask, returns the previous one.
 int set_cov_enabled(int mask);
-int env_items_per_wg();
-int set_env_items(int n);
 hipError_t launch_debug_mfma(const double* a, const double* b, double* c, hipStream_t s);
 
 // Launch geometry of the envelope stage for (B, S): waves per workgroup and

@@ -572,22 +572,6 @@ static bool cov_big(int N, int B, int m) {
 // The opt-in covariance block kernels (bits: DKG_COV_ENABLE_BLK / _REC2 / _REG), enabled by their environment
 // variables (DKG_COV_BLK / DKG_COV_REC2 / DKG_COV_REG) or by dkg_debug_cov_kernels (tests: each gives the narrow
 // kernel's bits, checked by tests/test_gpu_batches.py with it enabled).
-// Candidates per workgroup of the staged forward envelope (envelope_kernel's ipw): 1 unless DKG_ENV_IPW (A/B) or
-// dkg_debug_env_items (tests: every value gives the same bits) sets it.
-static int g_env_ipw = -1;  // -1: from the environment at first use
-int env_items_per_wg() {
-  if (g_env_ipw < 0) {
-    const char* e = std::getenv("DKG_ENV_IPW");
-    g_env_ipw = e ? std::max(1, std::min(8, std::atoi(e))) : 1;
-  }
-  return g_env_ipw;
-}
-int set_env_items(int n) {
-  const int prev = env_items_per_wg();
-  g_env_ipw = std::max(1, std::min(8, n));
-  return prev;
-}
-
 static int g_cov_enable = -1;  // -1: from the environment at first use
 static int cov_enabled() {
   if (g_cov_enable < 0) {
@@ -825,7 +809,7 @@ hipError_t launch_stage(const Plan& h, const Plan* dev, const double* xnew, int 
   }
   EnvLaunch a{&h, dev, B, kg, pairs, dim3(xcd_group_size(B, h.split)), dim3(h.sw * WAVE),
               envelope_lds_bytes(h.m, h.N, h.sw, h.S, h.stream != 0, false, !DKG_ICP), s, h.debug_stamp, nullptr,
-              nullptr, nullptr, env_items_per_wg()};
+              nullptr};
   return launch_env<false>(h, a);
 }
 

@@ -103,7 +103,6 @@ SIGNATURES = {
     "dkg_debug_read_kstamps": (c_int, [c_void_p, c_int]),
     "dkg_debug_wave_ops": (c_int, [c_void_p, c_void_p, c_void_p]),
     "dkg_debug_cov_kernels": (c_int, [c_int]),
-    "dkg_debug_env_items": (c_int, [c_int]),
     "dkg_debug_mfma_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 

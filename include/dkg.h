@@ -330,12 +330,6 @@ int dkg_debug_mfma_f64(const double* a, const double* b, double* c, void* stream
 #define DKG_COV_ENABLE_REG 4  /* register-operand blocks, any m, one 8-wave workgroup per CU */
 int dkg_debug_cov_kernels(int mask);
 
-/* Test/A-B hook: candidates per workgroup of the staged forward's envelope stage (1..8; the DKG_ENV_IPW
- * environment variable sets the initial value, default 1).  A workgroup then stages mu_D once and runs its
- * candidates in turn, the next one's covariance records DMA'd while the current one's pairs run.  Every value
- * gives the same bits.  n < 0 reads the current value; otherwise sets it and returns the previous one. */
-int dkg_debug_env_items(int n);
-
 /* ---- Launcher: captured forward graphs of several streams enqueued side by side from host threads.
  * A hipGraphLaunch costs ~1 us of host time per kernel node plus ~9 us; one thread launching every
  * stream's graphs in turn leaves the last stream idle for the others' launches.  The
