@@ -83,7 +83,10 @@ __host__ __device__ inline int cross_groups(int np, int d) {
   return ((np / 16 + 1) / 2 + cross_pairs(np, d) - 1) / cross_pairs(np, d);
 }
 constexpr int KF_WAVES = 4;
-constexpr int KF_KB = 16;  // k-blocks (of 4 columns) per fill workgroup
+#ifndef DKG_KF_KB
+#define DKG_KF_KB 16
+#endif
+constexpr int KF_KB = DKG_KF_KB;  // k-blocks (of 4 columns) per fill workgroup
 
 // Pre-scaled r^2 and the kernel term exactly as cross_root_impl's fill evaluates them (same operations,
 // same order), so a loaded entry is the bits the fill would have produced.  Compiled without FP contraction
