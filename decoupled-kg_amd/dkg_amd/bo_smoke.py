@@ -15,9 +15,11 @@ What it restates (reference files, read for behaviour only):
   training set; full, ``optimize_for_full_evaluation`` picks x and every objective is evaluated;
 * ``modules/gp_testproblem.py:76-98``: the objective of a ``gp-sample`` problem is the posterior
   mean of the problem GP, evaluated here on the device (``dkg_prepare_output`` + ``dkg_cross_root``);
-* the ``fit_hyperparams = never`` model path (``bo_loop.py:574-619``): the problem's fixed
-  hyperparameters, noise at the 1e-8 floor.  Hyperparameter fitting (``fit_gpytorch_mll``) is not
-  restated: it is outside the KG path.
+* the model paths of ``bo_loop.py:574-619``: ``never`` (the problem's fixed hyperparameters, noise at the
+  1e-8 floor), ``once`` (MAP hyperparameters fitted once on 1000 Sobol points of the problem,
+  ``fit_hyperparameters``, ``:63-79``) and ``always`` (refitted on the observations at every iteration, the
+  constant means kept at the first fit's); the fit is ``dkg_amd.fit.fit_map`` (parity unpinned: GPyTorch /
+  BoTorch are absent here), the fitted paths' noise ``MIN_NOISE_SE**2`` (``fix_zero_noise``).
 
 Scalarisation weights are drawn per step with the reference's qMC simplex sampler
 (``bo_loop.py:84-118``, ``dkg_amd.utils.sample_simplex``).
@@ -58,7 +60,7 @@ def _output_config(lengthscale_rate: float) -> dict:
             "standardize_output": False}
 
 
-def reference_model_config(m: int, bounds) -> dict:
+def reference_model_config(m: int, bounds, fit_hyperparams: str = "never") -> dict:
     """The ``model_config`` the reference's SMOKE run checkpoints (``bo_loop.py:281-290``): the ``model``
     section of ``config/experiment-lengthscales.yaml`` (the ``gp-sample:lengthscales`` problem), completed
     as ``pipeline/cli.py:22-37`` does for ``--fit-hyperparams never`` (``fit_hyperparams``, and
@@ -67,7 +69,7 @@ def reference_model_config(m: int, bounds) -> dict:
     the config's two repeat its second output's section.  Pinned by tests/golden/ref_schema.json."""
     bnd = torch.as_tensor(bounds, dtype=torch.double).reshape(2, -1)
     return {"bounds": bnd.tolist(), "outputs": [_output_config(10 if i == 0 else 1.1) for i in range(m)],
-            "fit_hyperparams": "never"}
+            "fit_hyperparams": fit_hyperparams}
 QUERY_COLUMNS = ("iteration", "x", "obj_index", "obj", "obj_true", "cost", "acq_per_cost", "init", "scalarisation")
 
 
@@ -97,21 +99,40 @@ class GPProblem:
 def surrogate(train_x: Sequence[Tensor], train_y: Sequence[Tensor], hyper: Dict[str, Sequence[float]],
               noise: float = NEVER_FIT_NOISE) -> ModelListGPState:
     """The BO model on the observations so far, one output per objective with its own data
-    (decoupled evaluations give every objective its own training set), fixed hyperparameters."""
+    (decoupled evaluations give every objective its own training set), fixed hyperparameters; the noise is
+    ``hyper["noises"][i]`` when the hyperparameters were fitted, else ``noise``."""
+    noises = hyper.get("noises") or [noise] * len(train_x)
     outs = [SingleTaskGPState(train_x[i], train_y[i], torch.tensor(hyper["length_scales"][i], dtype=torch.double),
-                              float(hyper["output_scales"][i]), noise, float(hyper["means"][i]))
+                              float(hyper["output_scales"][i]), float(noises[i]), float(hyper["means"][i]))
             for i in range(len(train_x))]
     return ModelListGPState(*outs)
+
+
+def fit_hyperparameters(problem: "GPProblem", model_config: dict, n: int = 1000) -> Dict[str, list]:
+    """``bo_loop.fit_hyperparameters`` (``:63-79``): n Sobol points of the problem (global RNG, as
+    ``draw_sobol_samples`` without a seed), every objective evaluated there, the MAP fit of the surrogate
+    (``dkg_amd.fit.fit_map``)."""
+    from .fit import fit_map
+
+    x = draw_sobol_samples(problem.bounds, n, 1).squeeze(-2)
+    y = problem(x)
+    return fit_map([x] * problem.num_objectives, [y[:, i] for i in range(problem.num_objectives)], model_config)
 
 
 def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bool, n_iter: int = 2,
              n_init: int = 6, costs: Sequence[float] = (1, 10), n_scalarisations: int = 16,
              spec: Optional[DiscreteKgOptimisationSpec] = None, seed: int = 0,
-             catalog: Optional[DataCatalog] = None, run_key: Optional[str] = None) -> Dict[str, List]:
+             catalog: Optional[DataCatalog] = None, run_key: Optional[str] = None,
+             fit_hyperparams: str = "never") -> Dict[str, List]:
     """``bo_loop.run_mobo`` with the discrete-KG strategy for ``n_iter`` BO steps; returns the
     query history (x, objective index or None for full evaluation, observed values, acquisition).
     With ``catalog`` it also writes the reference's checkpoints and query-history table under
-    ``run_key`` (default ``eval_separate`` / ``eval_full``)."""
+    ``run_key`` (default ``eval_separate`` / ``eval_full``).  ``fit_hyperparams`` (``bo_loop.py:574-619``):
+    ``never`` and ``once`` use ``hyper`` as given (``once``: the fitted values with their ``noises``);
+    ``always`` refits on the observations before every model use, the constant means fixed at the first
+    fit's (``:600-614``)."""
+    if fit_hyperparams not in ("never", "once", "always"):
+        raise ValueError(f"Unexpected value for fit_hyperparams. Got {fit_hyperparams!r}")
     m, d = problem.num_objectives, problem.gp.input_dim
     # the pipeline's --seed (main.py:235, utils.set_random_seed): every later draw comes from the global RNG, as
     # in the reference -- the initial Sobol points (generate_initial_data, bo_loop.py:48-49: no seed), each
@@ -135,7 +156,19 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
                                         float(cost), acq_per_cost, init, w)):
             qh[k].append(v)
 
-    model_config = reference_model_config(m, problem.bounds)
+    model_config = reference_model_config(m, problem.bounds, fit_hyperparams)
+    fitted_means = None
+
+    def model_now(first: bool = False):
+        # the surrogate for the next step: refitted on the data so far on the `always` path
+        nonlocal hyper, fitted_means
+        if fit_hyperparams == "always":
+            from .fit import fit_map
+
+            hyper = fit_map(train_x, train_y, model_config, fixed_means=None if first else fitted_means)
+            if first:
+                fitted_means = list(hyper["means"])
+        return surrogate(train_x, train_y, hyper)
 
     def checkpoint(iteration, model):
         if catalog is not None:
@@ -146,10 +179,10 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
     for i in range(m):
         for j in range(n_init):
             record(0, x0[j].numpy(), i, y0[j, i], costs[i], float("nan"), True, None)
-    checkpoint(0, surrogate(train_x, train_y, hyper))
+    model = model_now(first=True)
+    checkpoint(0, model)
     for it in range(n_iter):
         W = sample_simplex(m, n_scalarisations, qmc=True, seed=seed + 1 + it, dtype=torch.double)
-        model = surrogate(train_x, train_y, hyper)
         w_row = W[0].numpy().copy() if W.shape[0] == 1 else None
         if separate:
             x, i, acq = spec.optimize_for_single_objective(model, costs, d, scalarisation_weights=W)
@@ -175,7 +208,8 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
                 record(it + 1, x[0].numpy(), i, y[i], costs[i], float(acq) / float(sum(costs)), False, w_row)
         hist["x"].append(x[0].tolist())
         hist["acq"].append(float(acq))
-        checkpoint(it + 1, surrogate(train_x, train_y, hyper))
+        model = model_now()
+        checkpoint(it + 1, model)
     hist["n_observations"] = [int(t.shape[0]) for t in train_x]
     hist["query_history"] = qh
     if catalog is not None:
@@ -187,8 +221,22 @@ def run_mobo(problem: GPProblem, hyper: Dict[str, Sequence[float]], separate: bo
 
 
 def run_smoke(problem: GPProblem, hyper: Dict[str, Sequence[float]], seed: int = 0,
-              catalog: Optional[DataCatalog] = None) -> Dict[str, Dict]:
+              catalog: Optional[DataCatalog] = None, fit_hyperparams: str = "never") -> Dict[str, Dict]:
     """``run_pipeline`` under ``SMOKE_TEST`` (``main.py:171-216``): the separate-evaluation run and
-    the full-evaluation run, two BO steps each; with ``catalog`` both write the reference's files."""
-    return {"separate": run_mobo(problem, hyper, separate=True, seed=seed, catalog=catalog),
-            "full": run_mobo(problem, hyper, separate=False, seed=seed, catalog=catalog)}
+    the full-evaluation run, two BO steps each; with ``catalog`` both write the reference's files.
+    ``fit_hyperparams = "once"`` fits the hyperparameters first (``main.py:181-182``, saved to the catalog's
+    ``hyperparameters.pt`` as the fitted surrogate's state dict) and both runs use them; ``"always"`` refits
+    inside the runs."""
+    if fit_hyperparams == "once":
+        torch.manual_seed(seed)
+        cfg = reference_model_config(problem.num_objectives, problem.bounds, "once")
+        hyper = fit_hyperparameters(problem, cfg)
+        if catalog is not None:
+            x = torch.zeros(1, problem.gp.input_dim, dtype=torch.double)
+            y = torch.zeros(1, dtype=torch.double)
+            catalog.save_model_hyperparameters(
+                to_state_dict(surrogate([x] * problem.num_objectives, [y] * problem.num_objectives, hyper), cfg))
+    return {"separate": run_mobo(problem, hyper, separate=True, seed=seed, catalog=catalog,
+                                 fit_hyperparams=fit_hyperparams),
+            "full": run_mobo(problem, hyper, separate=False, seed=seed, catalog=catalog,
+                             fit_hyperparams=fit_hyperparams)}

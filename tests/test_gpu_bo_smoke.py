@@ -150,3 +150,30 @@ def test_smoke_pipeline_matches_the_oracle_run(seed, monkeypatch):
             assert g["x"][k] == pytest.approx(w["x"][k], abs=2e-3), (mode, k, g["x"][k], w["x"][k])
             assert g["acq"][k] == pytest.approx(w["acq"][k], rel=1e-4, abs=1e-8), (mode, k)
         assert all(a > 0 for a in g["acq"])
+
+
+@pytest.mark.parametrize("mode", ["once", "always"])
+def test_smoke_pipeline_fitted_hyperparameters(mode, tmp_path):
+    """The fitted model paths (bo_loop.py:63-79, 589-619; dkg_amd.fit): `once` fits on 1000 Sobol points of
+    the problem and saves the fitted state dict; `always` refits every iteration with the first fit's constant
+    means.  Both runs complete with finite acquisition values, and every checkpoint carries the fitted paths'
+    noise (MIN_NOISE_SE**2, fix_zero_noise) and the fitted hyperparameters."""
+    from dkg_amd.catalog import DataCatalog
+
+    state, *_ = load_golden("lengthscales0")
+    cat = DataCatalog("fit_" + mode, data_dir=str(tmp_path))
+    res = run_smoke(GPProblem(state, device=DEV), HYPER, seed=0, catalog=cat, fit_hyperparams=mode)
+    for h in (res["separate"], res["full"]):
+        assert len(h["x"]) == 2 and all(a == a and a >= 0.0 for a in h["acq"])
+    if mode == "once":
+        sd = cat.load_model_hyperparameters()
+        assert float(sd["models.0.likelihood.noise_covar.raw_noise"]) == pytest.approx(1e-4)
+    for key in ("eval_separate", "eval_full"):
+        cat.uncompress_checkpoints(key)
+        ck = cat.load_checkpoint(key, 2)
+        sd = ck["model_state_dict"]
+        assert float(sd["models.1.likelihood.noise_covar.raw_noise"]) == pytest.approx(1e-4)
+        assert ck["model_config"]["fit_hyperparams"] == mode
+        # fitted, not the problem's fixed lengthscales (0.2 / 1.8 under softplus)
+        raw = sd["models.0.covar_module.base_kernel.raw_lengthscale"]
+        assert not torch.allclose(torch.nn.functional.softplus(raw), torch.tensor([[0.2, 0.2]], dtype=torch.double))
