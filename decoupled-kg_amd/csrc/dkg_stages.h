@@ -813,7 +813,10 @@ __device__ __forceinline__ uint32_t big_block_terms(const Plan* __restrict__ P, 
 constexpr int PB_WAVES = 4;
 constexpr int PB_RT = 4;  // candidate tiles per block
 constexpr int PB_CT = 4;  // line tiles per block
-constexpr int PB_WC = 2;  // words (two k-blocks each) per staged chunk; even, so chains restart in step
+#ifndef DKG_PB_WC
+#define DKG_PB_WC 2
+#endif
+constexpr int PB_WC = DKG_PB_WC;  // words (two k-blocks each) per staged chunk (2 or 4); even, so chains restart in step
 // the kernel terms in registers (16 per lane) instead of parked in LDS: the LDS then holds the stage buffers only
 #ifndef DKG_PB_KVREG
 #define DKG_PB_KVREG 0
@@ -857,7 +860,8 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   // buffers apart).  Every wave issues PB_PIECES DMA instructions per chunk (words past a chunk's end repeat
   // a live word, unused), so the chunk-c wait is vmcnt <= PB_PIECES x (chunks issued after it).
   constexpr int PB_PIECES = (PB_RT + PB_CT) * PB_WC / PB_WAVES;
-  static_assert((PB_RT + PB_CT) * PB_WC % PB_WAVES == 0 && PB_PIECES == 4, "four DMA pieces per wave per chunk");
+  static_assert((PB_RT + PB_CT) * PB_WC % PB_WAVES == 0 && (PB_PIECES == 4 || PB_PIECES == 8),
+                "four or eight DMA pieces per wave per chunk");
   auto stage = [&](int c) {
     const int j0 = chunk_start(c), nw = chunk_words(c);
     double2* buf = stg + (size_t)(c % PB_NSTG) * PB_STAGE;
@@ -912,9 +916,12 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
   for (int c = 0; c < nc; ++c) {
     // chunk c landed (this wave's pieces), then every wave's: the later chunks' DMAs stay in flight
     const int later = min(nc - 1 - c, PB_NSTG - 2);  // chunks issued after c (wave-uniform)
-    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    switch (later * PB_PIECES) {
+      case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
     // a bare s_barrier: __syncthreads()'s workgroup fence would make the compiler drain every DMA in flight
     // (vmcnt(0)) first; LDS needs no fence within the workgroup once the DMA has landed (vmcnt above)
     asm volatile("s_barrier" ::: "memory");
@@ -943,26 +950,14 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
     const uint32_t so = (uint32_t)(c % PB_NSTG) * (uint32_t)(PB_STAGE * 16);
     const uint32_t aA = addrA + so, aB = addrB + so;
     const int nw = chunk_words(c);
-    // the chunk's two words in two register sets (no copies between them: a VALU copy into registers an
-    // MFMA group just read holds the next group until that group has read them): word 1's read is issued
-    // before word 0's MFMAs, and LDS reads complete in order, so lgkmcnt(4) means word 0 has landed
-    static_assert(PB_WC == 2, "two words per chunk: register sets X and Y");
+    // the chunk's words in pairs, each pair in two register sets X and Y (no copies between them: a VALU copy into
+    // registers an MFMA group just read holds the next group until that group has read them): word 2p + 1's read
+    // is issued before word 2p's MFMAs, and LDS reads complete in order, so lgkmcnt(4) means word 2p has landed.
+    // Set Y is read and waited for on every pair, a chunk's words past nw included (their slots repeat a live
+    // word, stage()): no branch between an asm read and its wait, where the register allocator would be free to
+    // copy the destination registers before the data lands (tools/asm_audit.py checks the compiled kernel).
+    static_assert(PB_WC % 2 == 0, "words in pairs: register sets X and Y");
     v2d xa0, xa1, xb0, xb1, ya0, ya1, yb0, yb1;
-    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:%6\n\tds_read_b128 %2, %5\n\t"
-                 "ds_read_b128 %3, %5 offset:%6"
-                 : "=&v"(xa0), "=&v"(xa1), "=&v"(xb0), "=&v"(xb1)
-                 : "v"(aA), "v"(aB), "i"(PB_WC * 1024)
-                 : "memory");
-    // Set Y is read and waited for on every chunk, a one-word chunk included (its word-1 slots repeat word 0,
-    // stage()): no branch between an asm read and its wait, where the register allocator would be free to copy
-    // the destination registers before the data lands (tools/asm_audit.py checks the compiled kernel for that)
-    const bool two = nw > 1;  // wave-uniform
-    asm volatile("ds_read_b128 %0, %4 offset:1024\n\tds_read_b128 %1, %4 offset:%6\n\t"
-                 "ds_read_b128 %2, %5 offset:1024\n\tds_read_b128 %3, %5 offset:%6"
-                 : "=&v"(ya0), "=&v"(ya1), "=&v"(yb0), "=&v"(yb1)
-                 : "v"(aA), "v"(aB), "i"((PB_WC + 1) * 1024)
-                 : "memory");
-    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa0), "+v"(xa1), "+v"(xb0), "+v"(xb1));
     auto word = [&](const v2d& a0, const v2d& a1, const v2d& b0, const v2d& b1, auto chc) __attribute__((always_inline)) {
       constexpr int chx = decltype(chc)::value;  // k-blocks 2 j, 2 j + 1 of the half: chains chx, chx + 1
       acc[0][0][chx] = mfma_f64(a0.x, b0.x, acc[0][0][chx]);
@@ -980,10 +975,48 @@ __global__ __launch_bounds__(PB_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu
         qsq[1] = fma(a1.y, a1.y, qsq[1]);
       }
     };
-    word(xa0, xa1, xb0, xb1, std::integral_constant<int, 0>{});
-    __builtin_amdgcn_sched_barrier(0);  // set X's MFMAs issue before set Y's wait (they hide its latency)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ya0), "+v"(ya1), "+v"(yb0), "+v"(yb1));
-    if (two) word(ya0, ya1, yb0, yb1, std::integral_constant<int, 2>{});
+    // Word g of the chunk goes through set X (g even) or Y (g odd).  Words 0 and 1 are read at the chunk start;
+    // word g + 2 is read right after word g's MFMAs have issued (into the same set, sixteen wait states later),
+    // so its LDS latency runs under word g + 1's MFMAs.  Before word g's MFMAs at most words g and g + 1 are in
+    // flight (LDS reads complete in order): lgkmcnt(4) has word g, lgkmcnt(0) the chunk's last word.
+    constexpr int TS = PB_WC * 1024;  // bytes between a wave's two tiles of one operand in a stage buffer
+    auto rd = [](v2d& a0, v2d& a1, v2d& b0, v2d& b1, uint32_t pA, uint32_t pB, auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (g < 2) {
+        asm volatile("ds_read_b128 %0, %4 offset:%6\n\tds_read_b128 %1, %4 offset:%7\n\t"
+                     "ds_read_b128 %2, %5 offset:%6\n\tds_read_b128 %3, %5 offset:%7"
+                     : "=&v"(a0), "=&v"(a1), "=&v"(b0), "=&v"(b1)
+                     : "v"(pA), "v"(pB), "i"(g * 1024), "i"(g * 1024 + TS)
+                     : "memory");
+      } else {
+        asm volatile("s_nop 7\n\ts_nop 7\n\tds_read_b128 %0, %4 offset:%6\n\tds_read_b128 %1, %4 offset:%7\n\t"
+                     "ds_read_b128 %2, %5 offset:%6\n\tds_read_b128 %3, %5 offset:%7"
+                     : "=&v"(a0), "=&v"(a1), "=&v"(b0), "=&v"(b1)
+                     : "v"(pA), "v"(pB), "i"(g * 1024), "i"(g * 1024 + TS)
+                     : "memory");
+      }
+    };
+    rd(xa0, xa1, xb0, xb1, aA, aB, std::integral_constant<int, 0>{});
+    rd(ya0, ya1, yb0, yb1, aA, aB, std::integral_constant<int, 1>{});
+    auto group = [&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      v2d& a0 = (g & 1) ? ya0 : xa0;
+      v2d& a1 = (g & 1) ? ya1 : xa1;
+      v2d& b0 = (g & 1) ? yb0 : xb0;
+      v2d& b1 = (g & 1) ? yb1 : xb1;
+      if constexpr (g + 1 < PB_WC) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
+      if (g < nw) word(a0, a1, b0, b1, std::integral_constant<int, (g & 1) ? 2 : 0>{});  // wave-uniform
+      __builtin_amdgcn_sched_barrier(0);  // the MFMAs issue before the next wait or rewrite
+      if constexpr (g + 2 < PB_WC) rd(a0, a1, b0, b1, aA, aB, std::integral_constant<int, g + 2>{});
+    };
+    group(std::integral_constant<int, 0>{});
+    group(std::integral_constant<int, 1>{});
+    if constexpr (PB_WC > 2) {
+      group(std::integral_constant<int, 2>{});
+      group(std::integral_constant<int, 3>{});
+    }
+    static_assert(PB_WC == 2 || PB_WC == 4, "two or four words per chunk");
     // Both sets' MFMAs issue here, before the next chunk's wait, barrier and fragment reads: the rewrites of
     // sets X and Y are inline asm, which the scheduler may otherwise move the (memory-free) MFMA builtins
     // across, and which the hazard recognizer does not see.  A scheduling barrier holds the order.
